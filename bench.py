@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X get_cliques hot path (BASELINE.json metric: micrographs/s).
+
+A "step" is one pass of the whole hot path (bin -> JI pairs -> graph/CC -> k-cliques +
+ILP epilogue -> constraint-matrix rows) over one batch of synthetic micrographs already
+resident in HBM.  Default workload = BASELINE.json configs[1] (C2: 10k micrographs x 3
+pickers x ~300 boxes, box 180, 4096^2) per GPU; multi-GPU runs shard micrographs across
+ranks (weak scaling, no collective in the hot path).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5] [--n_mg M]
+
+Prints ONE JSON line on rank 0 (driver contract), with "roofline" (dominant kernel, HIP
+events over the timed region) and "cpu_baseline" (the oracle's faithful per-pair loop on
+a bounded sample, 1 core).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "repic-copy_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+DEFAULT_MG = {"C2": 10000, "C3": 1000, "C4": 12500, "C5": 8}
+
+
+def alg_bytes(name, N, E, C, k, V):
+    """Algorithmic (compulsory) HBM bytes of one launch of each kernel."""
+    table = {
+        "k1_bin": 16 * N + 30 * N,                       # read x,y; write sorted SoA + maps
+        "k2_pairs_count": 21 * N + 4 * N,                # read sx,sy,spick,sbox; write count
+        "k2_pairs_fill": 21 * N + 8 * N + 12 * E,        # + offsets; write (dst, JI) per edge
+        "k4_union": 8 * N + 4 * E + 1 * N,               # offsets, targets, node flags
+        "k4_compress": 1 * N + 8 * N,                    # flags, parent read/write
+        "k4_stats": 1 * N + 8 * N,
+        "k5_cliques_count": 13 * N + 12 * E + 4 * N,     # roots' CSR walk; write counts
+        "k5_cliques_fill": 13 * N + 12 * E + 24 * V + C * (5 * k + 12),
+        "k7_rank": 1 * N + 20 * V,
+        "k7_rows": 12 * k * C,
+    }
+    return table.get(name)
+
+
+def pipeline_bytes(N, E, C, k):
+    """B_alg = 28 N + 32 E + C (20 k + 12) for the whole hot path."""
+    return 28 * N + 32 * E + C * (20 * k + 12)
+
+
+def cpu_baseline(cfg, mgs, budget_s=12.0):
+    """Oracle faithful per-pair loop (oracle/cpu_ref.py, same structure as the reference's
+    get_jaccard, get_cliques.py:59-69) on the first micrographs of this workload."""
+    from oracle import cpu_ref
+    methods = [f"picker{p}" for p in range(cfg.k)]
+    t0 = time.perf_counter()
+    n, nid = 0, 0
+    for mg in mgs:
+        coords = []
+        for (x, y, s) in mg:
+            coords.append([(float(a), float(b), float(c), nid + i)
+                           for i, (a, b, c) in enumerate(zip(x.tolist(), y.tolist(), s.tolist()))])
+            nid += len(x)
+        cpu_ref.micrograph(coords, cfg.box, methods, faithful=True)
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "micrographs/s", "cores": 1, "kind": "port",
+            "sample": f"{n} micrographs of this workload, oracle faithful per-pair loop "
+                      f"(reference get_jaccard structure), 1 process, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--n_mg", type=int, default=None, help="micrographs per GPU")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from repic_amd import _lib, synth
+    from repic_amd.pipeline import Batch
+
+    cfg = synth.SynthConfig(**synth.CONFIGS[args.config], seed=args.seed)
+    n_mg = args.n_mg or DEFAULT_MG[args.config]
+    t_gen = time.time()
+    mgs = synth.batch(cfg, n_mg, start=rank * n_mg)    # this rank's shard of one big batch
+    batch = Batch.pack(cfg.k, cfg.box, mgs)
+    t_gen = time.time() - t_gen
+    # the one exchange of the sharded path: global box-id offsets
+    if dist is not None:
+        tot = torch.tensor([batch.n_boxes], dtype=torch.int64, device=dev)
+        allt = [torch.zeros_like(tot) for _ in range(world)]
+        dist.all_gather(allt, tot)
+        id_off = int(sum(int(t.item()) for t in allt[:rank]))
+        batch.id_base = batch.id_base + id_off
+
+    # inputs resident in HBM (torch only for the allocation / handoff)
+    dx = torch.from_numpy(batch.x).to(dev)
+    dy = torch.from_numpy(batch.y).to(dev)
+    ds = torch.from_numpy(batch.score).to(dev)
+    torch.cuda.synchronize()
+    ctx = _lib.Context(local, torch.cuda.current_stream(dev).cuda_stream)
+    flags = _lib.F_DEVICE_INPUTS
+
+    def step(timing=False):
+        return ctx.run(batch.n_mg, cfg.k, cfg.box, batch.box_off, batch.id_base,
+                       dx.data_ptr(), dy.data_ptr(), ds.data_ptr(),
+                       flags | (_lib.F_TIMING if timing else 0))
+
+    for _ in range(args.warmup):
+        r = step()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ktimes = {}
+    for _ in range(args.steps):
+        r = step(timing=True)
+        for name, ms in ctx.kernel_times():
+            ktimes[name] = ktimes.get(name, 0.0) + ms
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    N, E, C = int(r.n_boxes), int(r.n_edges), int(r.n_cliques)
+    V = int(r.n_vert.sum())
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        # single end-of-run reduction of node-level counts over RCCL/xGMI
+        cnt = torch.tensor([n_mg, E, C], dtype=torch.int64, device=dev)
+        dist.all_reduce(cnt)
+        tot_mg, tot_e, tot_c = (int(v) for v in cnt.tolist())
+    else:
+        tot_mg, tot_e, tot_c = n_mg, E, C
+
+    steps = args.steps
+    value = tot_mg * steps / elapsed
+    avg = {k_: v / steps for k_, v in ktimes.items()}
+    kern = {k_: v for k_, v in avg.items() if alg_bytes(k_, N, E, C, cfg.k, V) is not None}
+    dom = max(kern, key=kern.get)
+    dom_bytes = alg_bytes(dom, N, E, C, cfg.k, V)
+    achieved = dom_bytes / (avg[dom] * 1e-3) / 1e9
+    dev_ms = sum(v for k_, v in avg.items() if k_ not in ("d2h", "h2d_meta"))
+    pipe = pipeline_bytes(N, E, C, cfg.k)
+    out = {
+        "metric": "micrographs/sec (get_cliques, whole node) at 1/2/4/8 MI355X; % HBM roofline",
+        "value": value, "unit": "micrographs/s", "n_gpus": world, "steps": steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64", "data": "synthetic (seeded SURVEY.md §8(d) generator)",
+        "config": {"workload": f"{args.config}: {synth.CONFIGS[args.config]}",
+                   "micrographs_per_gpu": n_mg, "k": cfg.k, "box_size": cfg.box,
+                   "boxes_per_gpu": N, "edges_per_gpu": E, "cliques_per_gpu": C,
+                   "parallelism": f"dp{world} (micrograph shards)"},
+        "edges_per_sec": tot_e * steps / elapsed,
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": None, "alg_bytes_per_launch": dom_bytes,
+                     "avg_launch_ms": avg[dom]},
+        "pipeline": {"device_ms_per_step": dev_ms, "alg_bytes": pipe,
+                     "achieved_gbs": pipe / (dev_ms * 1e-3) / 1e9,
+                     "frac": pipe / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "kernel_ms": {k_: round(v, 4) for k_, v in sorted(avg.items())}},
+        "gen_s": t_gen,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cfg, mgs, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

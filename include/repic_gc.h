@@ -1,0 +1,117 @@
+/* repic_gc.h — C-ABI of librepic_gc.so, the MI355X-native `repic get_cliques` hot path.
+ *
+ * The reference has no FFI: its boundary is the Python subcommand plugin protocol
+ * (`name`, `add_arguments(parser)`, `main(args)`; reference repic/commands/get_cliques.py
+ * :13-27,72 registered in repic/main.py:17-29).  The Python host package
+ * (repic-copy_amd/repic_amd/commands/get_cliques.py) keeps that protocol and calls the
+ * entry points below through ctypes.  Each entry point replaces one stage of the
+ * reference's per-micrograph loop (get_cliques.py:108-229):
+ *
+ *   rgc_parse_files  <- common.py:71-114 get_box_coords (BOX text -> x, y, score)
+ *   rgc_run          <- get_cliques.py:134-202: Jaccard pairs (:40-69,:134-138), graph
+ *                       (:30-37,:142-143), connected components (:145-156), size-k
+ *                       cliques (:49-56,:160-161), ILP weight / confidence / consensus
+ *                       (:164-190) and constraint-matrix COO (:192-202), for a whole
+ *                       batch of micrographs at once.
+ *
+ * Conventions: plain pointers and sizes, no torch types.  Returns 0 on success and a
+ * negative code on error (message in rgc_last_error(), thread-local).  Outputs are owned
+ * by the context and stay valid until the next rgc_run on it or rgc_ctx_destroy.
+ */
+#ifndef REPIC_GC_H
+#define REPIC_GC_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RGC_ABI_VERSION 1
+
+/* flags for rgc_batch_in.flags */
+#define RGC_F_GET_CC         1u  /* --get_cc   (get_cliques.py:151-156) */
+#define RGC_F_MULTI_OUT      2u  /* --multi_out (get_cliques.py:175-178,206-213) */
+#define RGC_F_DEVICE_INPUTS  4u  /* x/y/score are device pointers (HBM-resident) */
+#define RGC_F_HOST_OUTPUTS   8u  /* copy per-clique outputs to pinned host memory */
+#define RGC_F_TIMING        16u  /* record per-kernel HIP events (rgc_kernel_times) */
+
+/* per-micrograph status (rgc_batch_out.status) */
+#define RGC_OK          0   /* outputs written as in get_cliques.py:215-229 */
+#define RGC_NO_EDGES    1   /* reference raises ValueError (np.max([]), :148) */
+#define RGC_NO_CLIQUES  2   /* reference raises UnboundLocalError (del clique, :203) */
+
+typedef struct rgc_ctx rgc_ctx;
+
+typedef struct rgc_batch_in {
+  int32_t n_mg;            /* micrographs in the batch */
+  int32_t k;               /* pickers (= clique size, get_cliques.py:160), 1..8 */
+  int64_t box_size;        /* CLI box_size (int pixels, get_cliques.py:22-23) */
+  uint32_t flags;
+  const int64_t* box_off;  /* HOST [n_mg*k+1]: boxes of (mg m, picker p) are
+                              [box_off[m*k+p], box_off[m*k+p+1]) in file order */
+  const int64_t* id_base;  /* HOST [n_mg]: global box id of the first box of each
+                              micrograph (common.py:23,108-112 counter) */
+  const double* x;         /* [N] box x (common.py:87), host or device per flags */
+  const double* y;         /* [N] box y */
+  const double* score;     /* [N] score, sigmoid already applied on host (common.py:92-94) */
+} rgc_batch_in;
+
+typedef struct rgc_batch_out {
+  int64_t n_boxes, n_edges, n_cliques;
+  /* per micrograph [n_mg], host memory */
+  int32_t* status;
+  int32_t* cc_max;         /* runtime.tsv column 2 (get_cliques.py:228) */
+  int32_t* cc_cnt;         /* runtime.tsv column 3 */
+  int32_t* n_nodes;        /* graph nodes (boxes with >= 1 edge) */
+  int32_t* n_vert;         /* constraint-matrix rows V (get_cliques.py:164) */
+  int64_t* n_edges_mg;     /* JI > 0.3 edges */
+  int64_t* clique_off;     /* [n_mg+1] cliques of mg m are [clique_off[m], clique_off[m+1]) */
+  /* per clique; host (RGC_F_HOST_OUTPUTS) or device pointers */
+  int32_t* rows;           /* [C*k] COO row indices of each clique column, ascending */
+  float* w;                /* [C] weight vector (get_cliques.py:188-190) */
+  float* conf;             /* [C] consensus confidences (:186-187) */
+  int32_t* consensus;      /* [C] global box index of the consensus box (:182-183) */
+  int32_t* members;        /* [C*k] global box index of each member, picker order */
+  uint8_t* order;          /* [C*k] networkx node-iteration order as picker indices
+                              (only with RGC_F_MULTI_OUT, else NULL) */
+} rgc_batch_out;
+
+typedef struct rgc_parsed {
+  int64_t n_files;
+  int32_t* status;         /* [n_files] RGC_PARSE_* */
+  int64_t* off;            /* [n_files+1] boxes of file f are [off[f], off[f+1]) */
+  double* x;
+  double* y;
+  double* score;           /* raw scores (sigmoid NOT applied) */
+  uint8_t* sigmoid;        /* [n_files] 1 if min(score) < 0 (common.py:92) */
+} rgc_parsed;
+
+/* rgc_parsed.status — the exception get_box_coords would raise for that file */
+#define RGC_PARSE_OK          0
+#define RGC_PARSE_INDEX       1  /* IndexError: empty file / blank first line / no coords */
+#define RGC_PARSE_VALUE       2  /* ValueError: shortest row != 5 tokens, bad weight */
+#define RGC_PARSE_ASSERT      3  /* AssertionError: len(X) != len(Y) */
+#define RGC_PARSE_FALLBACK    4  /* non-ASCII / unusual bytes: parse in Python instead */
+#define RGC_PARSE_OSERROR     5  /* could not open / read */
+
+int rgc_abi_version(void);
+const char* rgc_last_error(void);
+int rgc_device_count(int* n);
+
+int rgc_ctx_create(int device, void* hip_stream, rgc_ctx** out);
+void rgc_ctx_destroy(rgc_ctx* ctx);
+int rgc_run(rgc_ctx* ctx, const rgc_batch_in* in, rgc_batch_out* out);
+/* Per-kernel device milliseconds of the last rgc_run with RGC_F_TIMING; returns the count. */
+int rgc_kernel_times(rgc_ctx* ctx, int max_n, float* ms, const char** names);
+
+int rgc_parse_files(const char* const* paths, int64_t n_files, int n_threads, rgc_parsed** out);
+void rgc_parsed_free(rgc_parsed* p);
+
+/* Host test hooks for the CPython set-order emulation (pyset.h). */
+uint64_t rgc_py_hash_node(double x, double y, int64_t id);
+int rgc_py_set_order(const uint64_t* hashes, int n, int8_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,443 @@
+// rgc_abi.cpp — host orchestration of the batched get_cliques pipeline + the C-ABI
+// (include/repic_gc.h).  One context per device/stream; device workspace is a grow-only
+// arena so steady-state calls do no hipMalloc.  Data-dependent sizes (edges, cliques) are
+// resolved by two-phase count -> scan -> fill with one small D2H read per phase.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/repic_gc.h"
+#include "pyset.h"
+#include "rgc_kernels.h"
+
+using namespace rgc;
+
+static thread_local std::string g_err;
+
+static int fail(const std::string& msg) {
+  g_err = msg;
+  return -1;
+}
+#define HIPCHK(expr)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return fail(std::string(#expr) + ": " + hipGetErrorString(e_));                   \
+  } while (0)
+
+namespace {
+
+enum DevBufId {
+  D_BOXOFF, D_CELLOFF, D_IDBASE, D_X, D_Y, D_S, D_GRID, D_CELLSTART, D_SX, D_SY, D_SBOX,
+  D_SPICK, D_SMG, D_BMG, D_BPICK, D_FWDCNT, D_FWDOFF, D_TILES, D_TOTAL, D_EDST, D_EJI,
+  D_PARENT, D_HASEDGE, D_CSIZE, D_STAT, D_INSKEY, D_COMPMIN, D_CCOUNT, D_COFF, D_MEMBERS,
+  D_W, D_CONF, D_CONS, D_ORDER, D_INCL, D_VLIST, D_VSORT, D_VROW, D_ROWS, D_MGOFF, D_COUNT
+};
+enum HostBufId {
+  H_STAGE, H_TOTAL, H_STAT, H_MGOFF, H_ROWS, H_W, H_CONF, H_CONS, H_MEMBERS, H_ORDER, H_COUNT
+};
+
+struct Buf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
+}  // namespace
+
+struct rgc_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  Buf d[D_COUNT];
+  Buf h[H_COUNT];
+  std::vector<hipEvent_t> events;
+  std::vector<const char*> ev_names;
+  int n_ev = 0;
+  bool timing = false;
+  std::vector<float> times;
+  std::vector<const char*> time_names;
+  // per-micrograph host outputs
+  std::vector<int32_t> status, cc_max, cc_cnt, n_nodes, n_vert;
+  std::vector<int64_t> n_edges_mg, clique_off;
+};
+
+static int ensure_dev(rgc_ctx* c, int id, size_t bytes) {
+  Buf& b = c->d[id];
+  if (bytes == 0) bytes = 16;
+  if (b.cap >= bytes) return 0;
+  if (b.p) HIPCHK(hipFree(b.p));
+  size_t cap = std::max(bytes, b.cap + b.cap / 2);
+  cap = (cap + 255) & ~(size_t)255;
+  b.p = nullptr;
+  b.cap = 0;
+  HIPCHK(hipMalloc(&b.p, cap));
+  b.cap = cap;
+  return 0;
+}
+
+static int ensure_host(rgc_ctx* c, int id, size_t bytes) {
+  Buf& b = c->h[id];
+  if (bytes == 0) bytes = 16;
+  if (b.cap >= bytes) return 0;
+  if (b.p) HIPCHK(hipHostFree(b.p));
+  size_t cap = std::max(bytes, b.cap + b.cap / 2);
+  b.p = nullptr;
+  b.cap = 0;
+  HIPCHK(hipHostMalloc(&b.p, cap, hipHostMallocDefault));
+  b.cap = cap;
+  return 0;
+}
+
+template <typename T>
+static T* D(rgc_ctx* c, int id) { return reinterpret_cast<T*>(c->d[id].p); }
+template <typename T>
+static T* H(rgc_ctx* c, int id) { return reinterpret_cast<T*>(c->h[id].p); }
+
+static int mark(rgc_ctx* c, const char* name) {
+  if (!c->timing) return 0;
+  if (c->n_ev >= (int)c->events.size()) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    c->events.push_back(e);
+    c->ev_names.push_back(nullptr);
+  }
+  c->ev_names[c->n_ev] = name;
+  HIPCHK(hipEventRecord(c->events[c->n_ev], c->stream));
+  ++c->n_ev;
+  return 0;
+}
+
+#define TRY(expr)        \
+  do {                   \
+    int r_ = (expr);     \
+    if (r_ != 0) return r_; \
+  } while (0)
+
+static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
+  const int n_mg = in->n_mg, k = in->k;
+  const uint32_t flags = in->flags;
+  if (n_mg < 0) return fail("n_mg < 0");
+  if (k < 1 || k > MAX_K) return fail("k (number of pickers) must be in 1..8");
+  if (in->box_size > (1LL << 26)) return fail("box_size too large (> 2^26)");
+  const int64_t N = n_mg ? in->box_off[(int64_t)n_mg * k] : 0;
+  if (N >= (1LL << 31) - 1) return fail("too many boxes in one batch (>= 2^31)");
+  const int get_cc = (flags & RGC_F_GET_CC) ? 1 : 0;
+  const int multi = (flags & RGC_F_MULTI_OUT) ? 1 : 0;
+  const double B = (double)in->box_size;
+  const double two_b2 = (double)(2 * in->box_size * in->box_size);
+  c->timing = (flags & RGC_F_TIMING) != 0;
+  c->n_ev = 0;
+
+  c->status.assign(n_mg, 0);
+  c->cc_max.assign(n_mg, 0);
+  c->cc_cnt.assign(n_mg, 0);
+  c->n_nodes.assign(n_mg, 0);
+  c->n_vert.assign(n_mg, 0);
+  c->n_edges_mg.assign(n_mg, 0);
+  c->clique_off.assign(n_mg + 1, 0);
+  std::memset(out, 0, sizeof(*out));
+  out->status = c->status.data();
+  out->cc_max = c->cc_max.data();
+  out->cc_cnt = c->cc_cnt.data();
+  out->n_nodes = c->n_nodes.data();
+  out->n_vert = c->n_vert.data();
+  out->n_edges_mg = c->n_edges_mg.data();
+  out->clique_off = c->clique_off.data();
+  out->n_boxes = N;
+  if (n_mg == 0) return 0;
+  if (k == 1) {  // no picker pairs -> no edges -> reference ValueError on every micrograph
+    std::fill(c->status.begin(), c->status.end(), RGC_NO_EDGES);
+    return 0;
+  }
+
+  // ---- small per-micrograph arrays (host -> device through one pinned staging buffer)
+  const size_t nbo = (size_t)n_mg * k + 1;
+  std::vector<int32_t> cell_off(n_mg + 1);
+  int64_t cells = 0;
+  for (int m = 0; m < n_mg; ++m) {
+    cell_off[m] = (int32_t)cells;
+    const int64_t nm = in->box_off[(int64_t)(m + 1) * k] - in->box_off[(int64_t)m * k];
+    cells += std::min<int64_t>(nm + 1, CELL_CAP - 1) + 2;
+  }
+  cell_off[n_mg] = (int32_t)cells;
+  if (cells >= (1LL << 31)) return fail("too many grid cells in one batch");
+  const size_t stage_bytes = nbo * 4 + (n_mg + 1) * 4 + n_mg * 8 + 64;
+  TRY(ensure_host(c, H_STAGE, stage_bytes));
+  int32_t* st_bo = H<int32_t>(c, H_STAGE);
+  int32_t* st_co = st_bo + nbo;
+  int64_t* st_id = reinterpret_cast<int64_t*>(
+      (reinterpret_cast<uintptr_t>(st_co + n_mg + 1) + 7) & ~(uintptr_t)7);
+  for (size_t i = 0; i < nbo; ++i) st_bo[i] = (int32_t)in->box_off[i];
+  std::memcpy(st_co, cell_off.data(), (n_mg + 1) * 4);
+  std::memcpy(st_id, in->id_base, n_mg * 8);
+
+  TRY(ensure_dev(c, D_BOXOFF, nbo * 4));
+  TRY(ensure_dev(c, D_CELLOFF, (n_mg + 1) * 4));
+  TRY(ensure_dev(c, D_IDBASE, n_mg * 8));
+  TRY(ensure_dev(c, D_GRID, n_mg * sizeof(MgGrid)));
+  TRY(ensure_dev(c, D_CELLSTART, cells * 4));
+  TRY(ensure_dev(c, D_SX, N * 8));
+  TRY(ensure_dev(c, D_SY, N * 8));
+  TRY(ensure_dev(c, D_SBOX, N * 4));
+  TRY(ensure_dev(c, D_SPICK, N));
+  TRY(ensure_dev(c, D_SMG, N * 4));
+  TRY(ensure_dev(c, D_BMG, N * 4));
+  TRY(ensure_dev(c, D_BPICK, N));
+  TRY(ensure_dev(c, D_FWDCNT, N * 4));
+  TRY(ensure_dev(c, D_FWDOFF, (N + 1) * 8));
+  const int64_t ntile = scan_tiles_needed(N + 1);
+  TRY(ensure_dev(c, D_TILES, ntile * 8));
+  TRY(ensure_dev(c, D_TOTAL, 16));
+  TRY(ensure_dev(c, D_PARENT, N * 4));
+  TRY(ensure_dev(c, D_HASEDGE, N));
+  TRY(ensure_dev(c, D_CSIZE, N * 4));
+  TRY(ensure_dev(c, D_STAT, n_mg * sizeof(MgStat)));
+  TRY(ensure_dev(c, D_INSKEY, N * 8));
+  if (get_cc) TRY(ensure_dev(c, D_COMPMIN, N * 8));
+  TRY(ensure_dev(c, D_CCOUNT, N * 4));
+  TRY(ensure_dev(c, D_COFF, (N + 1) * 8));
+  TRY(ensure_dev(c, D_INCL, N));
+  TRY(ensure_dev(c, D_VLIST, N * 4));
+  TRY(ensure_dev(c, D_VSORT, N * 4));
+  TRY(ensure_dev(c, D_VROW, N * 4));
+  TRY(ensure_dev(c, D_MGOFF, (n_mg + 1) * 8));
+  TRY(ensure_host(c, H_TOTAL, 16));
+  TRY(ensure_host(c, H_STAT, n_mg * sizeof(MgStat)));
+  TRY(ensure_host(c, H_MGOFF, (n_mg + 1) * 8));
+
+  hipStream_t s = c->stream;
+  TRY(mark(c, "h2d_meta"));
+  HIPCHK(hipMemcpyAsync(D<void>(c, D_BOXOFF), st_bo, nbo * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(D<void>(c, D_CELLOFF), st_co, (n_mg + 1) * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(D<void>(c, D_IDBASE), st_id, n_mg * 8, hipMemcpyHostToDevice, s));
+  const double *x = in->x, *y = in->y, *sc = in->score;
+  if (!(flags & RGC_F_DEVICE_INPUTS)) {
+    TRY(ensure_dev(c, D_X, N * 8));
+    TRY(ensure_dev(c, D_Y, N * 8));
+    TRY(ensure_dev(c, D_S, N * 8));
+    HIPCHK(hipMemcpyAsync(D<void>(c, D_X), in->x, N * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(D<void>(c, D_Y), in->y, N * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(D<void>(c, D_S), in->score, N * 8, hipMemcpyHostToDevice, s));
+    x = D<double>(c, D_X);
+    y = D<double>(c, D_Y);
+    sc = D<double>(c, D_S);
+  }
+  TRY(mark(c, "memset"));
+  HIPCHK(hipMemsetAsync(D<void>(c, D_HASEDGE), 0, N, s));
+  HIPCHK(hipMemsetAsync(D<void>(c, D_CSIZE), 0, N * 4, s));
+  HIPCHK(hipMemsetAsync(D<void>(c, D_INCL), 0, N, s));
+  HIPCHK(hipMemsetAsync(D<void>(c, D_INSKEY), 0xff, N * 8, s));
+  if (get_cc) HIPCHK(hipMemsetAsync(D<void>(c, D_COMPMIN), 0xff, N * 8, s));
+
+  const int32_t* bo = D<int32_t>(c, D_BOXOFF);
+  TRY(mark(c, "k1_bin"));
+  launch_bin(s, n_mg, k, B, bo, D<int32_t>(c, D_CELLOFF), x, y, D<MgGrid>(c, D_GRID),
+             D<int32_t>(c, D_CELLSTART), D<double>(c, D_SX), D<double>(c, D_SY),
+             D<int32_t>(c, D_SBOX), D<uint8_t>(c, D_SPICK), D<int32_t>(c, D_SMG),
+             D<int32_t>(c, D_BMG), D<uint8_t>(c, D_BPICK));
+  TRY(mark(c, "k2_pairs_count"));
+  launch_pairs(s, false, (int)N, k, B, two_b2, bo, D<int32_t>(c, D_CELLOFF), D<MgGrid>(c, D_GRID),
+               D<int32_t>(c, D_CELLSTART), D<double>(c, D_SX), D<double>(c, D_SY),
+               D<int32_t>(c, D_SBOX), D<uint8_t>(c, D_SPICK), D<int32_t>(c, D_SMG),
+               D<int32_t>(c, D_FWDCNT), nullptr, nullptr, nullptr);
+  TRY(mark(c, "scan_edges"));
+  launch_scan(s, N, D<int32_t>(c, D_FWDCNT), D<int64_t>(c, D_FWDOFF), D<int64_t>(c, D_TILES),
+              D<int64_t>(c, D_TOTAL));
+  HIPCHK(hipMemcpyAsync(H<int64_t>(c, H_TOTAL), D<int64_t>(c, D_TOTAL), 8,
+                        hipMemcpyDeviceToHost, s));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));
+  const int64_t E = H<int64_t>(c, H_TOTAL)[0];
+  out->n_edges = E;
+  TRY(ensure_dev(c, D_EDST, E * 4));
+  TRY(ensure_dev(c, D_EJI, E * 8));
+  TRY(mark(c, "k2_pairs_fill"));
+  launch_pairs(s, true, (int)N, k, B, two_b2, bo, D<int32_t>(c, D_CELLOFF), D<MgGrid>(c, D_GRID),
+               D<int32_t>(c, D_CELLSTART), D<double>(c, D_SX), D<double>(c, D_SY),
+               D<int32_t>(c, D_SBOX), D<uint8_t>(c, D_SPICK), D<int32_t>(c, D_SMG),
+               D<int32_t>(c, D_FWDCNT), D<int64_t>(c, D_FWDOFF), D<int32_t>(c, D_EDST),
+               D<double>(c, D_EJI));
+
+  static const char* cc_names[7] = {"k4_init",     "k4_union",    "k4_compress", "k4_stats",
+                                    "k4_ins_keys", "k4_comp_min", "k4_target"};
+  for (int phase = 0; phase < 7; ++phase) {
+    if ((phase == 5 || phase == 6) && !get_cc) continue;
+    TRY(mark(c, cc_names[phase]));
+    launch_cc(s, phase, (int)N, n_mg, k, get_cc, bo, D<int32_t>(c, D_BMG), D<uint8_t>(c, D_BPICK),
+              D<int64_t>(c, D_FWDOFF), D<int32_t>(c, D_EDST), D<int32_t>(c, D_PARENT),
+              D<uint8_t>(c, D_HASEDGE), D<int32_t>(c, D_CSIZE), D<MgStat>(c, D_STAT),
+              D<unsigned long long>(c, D_INSKEY), D<unsigned long long>(c, D_COMPMIN));
+  }
+
+  CliqueArgsHost A;
+  A.k = k; A.flags = get_cc | (multi << 1); A.box_off = bo; A.id_base = D<int64_t>(c, D_IDBASE);
+  A.x = x; A.y = y; A.score = sc; A.bmg = D<int32_t>(c, D_BMG); A.bpick = D<uint8_t>(c, D_BPICK);
+  A.fwd_off = D<int64_t>(c, D_FWDOFF); A.e_dst = D<int32_t>(c, D_EDST); A.e_ji = D<double>(c, D_EJI);
+  A.parent = D<int32_t>(c, D_PARENT); A.st = D<MgStat>(c, D_STAT);
+  A.ins_key = D<unsigned long long>(c, D_INSKEY); A.clique_off = D<int64_t>(c, D_COFF);
+  A.ccount = D<int32_t>(c, D_CCOUNT); A.in_clique = D<uint8_t>(c, D_INCL);
+  A.members = nullptr; A.w = nullptr; A.conf = nullptr; A.consensus = nullptr; A.order = nullptr;
+  TRY(mark(c, "k5_cliques_count"));
+  if (launch_cliques(s, false, (int)N, A) != 0) return fail("unsupported k");
+  TRY(mark(c, "scan_cliques"));
+  launch_scan(s, N, D<int32_t>(c, D_CCOUNT), D<int64_t>(c, D_COFF), D<int64_t>(c, D_TILES),
+              D<int64_t>(c, D_TOTAL));
+  HIPCHK(hipMemcpyAsync(H<int64_t>(c, H_TOTAL), D<int64_t>(c, D_TOTAL), 8,
+                        hipMemcpyDeviceToHost, s));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));
+  const int64_t C = H<int64_t>(c, H_TOTAL)[0];
+  out->n_cliques = C;
+  TRY(ensure_dev(c, D_MEMBERS, C * k * 4));
+  TRY(ensure_dev(c, D_W, C * 4));
+  TRY(ensure_dev(c, D_CONF, C * 4));
+  TRY(ensure_dev(c, D_CONS, C * 4));
+  TRY(ensure_dev(c, D_ROWS, C * k * 4));
+  if (multi) TRY(ensure_dev(c, D_ORDER, C * k));
+  A.members = D<int32_t>(c, D_MEMBERS); A.w = D<float>(c, D_W); A.conf = D<float>(c, D_CONF);
+  A.consensus = D<int32_t>(c, D_CONS); A.order = multi ? D<uint8_t>(c, D_ORDER) : nullptr;
+  TRY(mark(c, "k5_cliques_fill"));
+  launch_cliques(s, true, (int)N, A);
+  TRY(mark(c, "k7_rank"));
+  launch_rank(s, n_mg, k, bo, x, y, D<uint8_t>(c, D_INCL), D<int32_t>(c, D_VLIST),
+              D<int32_t>(c, D_VSORT), D<int32_t>(c, D_VROW), D<MgStat>(c, D_STAT));
+  TRY(mark(c, "k7_rows"));
+  launch_rows(s, k, C, D<int32_t>(c, D_MEMBERS), D<int32_t>(c, D_VROW), D<int32_t>(c, D_ROWS));
+  TRY(mark(c, "k_mg_offsets"));
+  launch_mg_offsets(s, n_mg, k, bo, D<int64_t>(c, D_COFF), D<int64_t>(c, D_MGOFF));
+  TRY(mark(c, "d2h"));
+  HIPCHK(hipMemcpyAsync(H<void>(c, H_STAT), D<void>(c, D_STAT), n_mg * sizeof(MgStat),
+                        hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOFF), D<void>(c, D_MGOFF), (n_mg + 1) * 8,
+                        hipMemcpyDeviceToHost, s));
+  if (flags & RGC_F_HOST_OUTPUTS) {
+    TRY(ensure_host(c, H_ROWS, C * k * 4));
+    TRY(ensure_host(c, H_W, C * 4));
+    TRY(ensure_host(c, H_CONF, C * 4));
+    TRY(ensure_host(c, H_CONS, C * 4));
+    TRY(ensure_host(c, H_MEMBERS, C * k * 4));
+    if (multi) TRY(ensure_host(c, H_ORDER, C * k));
+    HIPCHK(hipMemcpyAsync(H<void>(c, H_ROWS), D<void>(c, D_ROWS), C * k * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(H<void>(c, H_W), D<void>(c, D_W), C * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(H<void>(c, H_CONF), D<void>(c, D_CONF), C * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(H<void>(c, H_CONS), D<void>(c, D_CONS), C * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(H<void>(c, H_MEMBERS), D<void>(c, D_MEMBERS), C * k * 4,
+                          hipMemcpyDeviceToHost, s));
+    if (multi)
+      HIPCHK(hipMemcpyAsync(H<void>(c, H_ORDER), D<void>(c, D_ORDER), C * k, hipMemcpyDeviceToHost, s));
+    out->rows = H<int32_t>(c, H_ROWS);
+    out->w = H<float>(c, H_W);
+    out->conf = H<float>(c, H_CONF);
+    out->consensus = H<int32_t>(c, H_CONS);
+    out->members = H<int32_t>(c, H_MEMBERS);
+    out->order = multi ? H<uint8_t>(c, H_ORDER) : nullptr;
+  } else {
+    out->rows = D<int32_t>(c, D_ROWS);
+    out->w = D<float>(c, D_W);
+    out->conf = D<float>(c, D_CONF);
+    out->consensus = D<int32_t>(c, D_CONS);
+    out->members = D<int32_t>(c, D_MEMBERS);
+    out->order = multi ? D<uint8_t>(c, D_ORDER) : nullptr;
+  }
+  TRY(mark(c, "end"));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));
+
+  const MgStat* st = H<MgStat>(c, H_STAT);
+  const int64_t* mo = H<int64_t>(c, H_MGOFF);
+  for (int m = 0; m < n_mg; ++m) {
+    c->status[m] = st[m].status;
+    c->cc_max[m] = st[m].cc_max;
+    c->cc_cnt[m] = st[m].cc_cnt;
+    c->n_nodes[m] = st[m].n_nodes;
+    c->n_vert[m] = st[m].n_vert;
+    c->n_edges_mg[m] = st[m].n_edges;
+    c->clique_off[m] = mo[m];
+    if (c->status[m] == RGC_OK && mo[m + 1] == mo[m]) c->status[m] = RGC_NO_CLIQUES;
+  }
+  c->clique_off[n_mg] = mo[n_mg];
+
+  if (c->timing) {
+    c->times.clear();
+    c->time_names.clear();
+    for (int i = 0; i + 1 < c->n_ev; ++i) {
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, c->events[i], c->events[i + 1]));
+      c->times.push_back(ms);
+      c->time_names.push_back(c->ev_names[i]);
+    }
+  }
+  return 0;
+}
+
+extern "C" {
+
+int rgc_abi_version(void) { return RGC_ABI_VERSION; }
+
+const char* rgc_last_error(void) { return g_err.c_str(); }
+
+int rgc_device_count(int* n) {
+  HIPCHK(hipGetDeviceCount(n));
+  return 0;
+}
+
+int rgc_ctx_create(int device, void* hip_stream, rgc_ctx** out) {
+  *out = nullptr;
+  HIPCHK(hipSetDevice(device));
+  rgc_ctx* c = new rgc_ctx();
+  c->device = device;
+  if (hip_stream) {
+    c->stream = reinterpret_cast<hipStream_t>(hip_stream);
+  } else {
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      delete c;
+      return fail(std::string("hipStreamCreate: ") + hipGetErrorString(e));
+    }
+    c->own_stream = true;
+  }
+  *out = c;
+  return 0;
+}
+
+void rgc_ctx_destroy(rgc_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& b : c->d)
+    if (b.p) (void)hipFree(b.p);
+  for (auto& b : c->h)
+    if (b.p) (void)hipHostFree(b.p);
+  for (auto e : c->events) (void)hipEventDestroy(e);
+  if (c->own_stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int rgc_run(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
+  if (!c || !in || !out) return fail("null argument");
+  HIPCHK(hipSetDevice(c->device));
+  return run_impl(c, in, out);
+}
+
+int rgc_kernel_times(rgc_ctx* c, int max_n, float* ms, const char** names) {
+  if (!c) return fail("null ctx");
+  const int n = std::min<int>(max_n, (int)c->times.size());
+  for (int i = 0; i < n; ++i) {
+    if (ms) ms[i] = c->times[i];
+    if (names) names[i] = c->time_names[i];
+  }
+  return (int)c->times.size();
+}
+
+uint64_t rgc_py_hash_node(double x, double y, int64_t id) { return pyset::hash_node(x, y, id); }
+
+int rgc_py_set_order(const uint64_t* hashes, int n, int8_t* out) {
+  if (n < 0 || n > 18) return fail("set_order supports 0..18 keys");
+  return pyset::set_order(hashes, n, out);
+}
+
+}  // extern "C"

@@ -1,0 +1,77 @@
+// rgc_kernels.h — device-side data structures and kernel launchers (see rgc_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rgc {
+
+constexpr int MAX_K = 8;            // largest picker count with a compiled clique kernel
+constexpr int CELL_CAP = 8192;      // LDS counters per micrograph grid (k1_bin)
+constexpr int RANK_BUCKETS = 4096;  // LDS x-buckets for the row ranking (k7_rank)
+constexpr int SCAN_TILE = 2048;     // elements per scan workgroup
+
+// Uniform grid of one micrograph: cells of side `cell` (>= box_size) over its bounding box.
+struct MgGrid {
+  double minx, miny, cell;
+  int gx, gy, ncell, pad;
+};
+
+// Per-micrograph results.
+struct MgStat {
+  int64_t n_edges;
+  int n_nodes, cc_cnt, cc_max, status, target, n_vert;
+};
+
+struct CliqueArgsHost {
+  int k;
+  int flags;                 // bit 0: --get_cc, bit 1: --multi_out
+  const int32_t* box_off;
+  const int64_t* id_base;
+  const double* x;
+  const double* y;
+  const double* score;
+  const int32_t* bmg;
+  const uint8_t* bpick;
+  const int64_t* fwd_off;
+  const int32_t* e_dst;
+  const double* e_ji;
+  const int32_t* parent;
+  const MgStat* st;
+  const unsigned long long* ins_key;
+  const int64_t* clique_off;
+  int32_t* ccount;
+  int32_t* members;
+  float* w;
+  float* conf;
+  int32_t* consensus;
+  uint8_t* order;
+  uint8_t* in_clique;
+};
+
+void launch_bin(hipStream_t stream, int n_mg, int k, double B, const int32_t* box_off,
+                const int32_t* cell_off, const double* x, const double* y, MgGrid* grid,
+                int32_t* cell_start, double* sx, double* sy, int32_t* sbox, uint8_t* spick,
+                int32_t* smg, int32_t* bmg, uint8_t* bpick);
+void launch_pairs(hipStream_t stream, bool fill, int N, int k, double B, double two_b2,
+                  const int32_t* box_off, const int32_t* cell_off, const MgGrid* grid,
+                  const int32_t* cell_start, const double* sx, const double* sy,
+                  const int32_t* sbox, const uint8_t* spick, const int32_t* smg,
+                  int32_t* fwd_cnt, const int64_t* fwd_off, int32_t* e_dst, double* e_ji);
+int64_t scan_tiles_needed(int64_t n);
+void launch_scan(hipStream_t stream, int64_t n, const int32_t* in, int64_t* out,
+                 int64_t* tile_buf, int64_t* total);
+void launch_cc(hipStream_t stream, int phase, int N, int n_mg, int k, int get_cc,
+               const int32_t* box_off, const int32_t* bmg, const uint8_t* bpick,
+               const int64_t* fwd_off, const int32_t* e_dst, int32_t* parent, uint8_t* has_edge,
+               int32_t* csize, MgStat* st, unsigned long long* ins_key,
+               unsigned long long* comp_min);
+int launch_cliques(hipStream_t stream, bool fill, int N, const CliqueArgsHost& h);
+void launch_rank(hipStream_t stream, int n_mg, int k, const int32_t* box_off, const double* x,
+                 const double* y, const uint8_t* in_clique, int32_t* vlist, int32_t* vsort,
+                 int32_t* vrow, MgStat* st);
+int launch_rows(hipStream_t stream, int k, int64_t C, const int32_t* members,
+                const int32_t* vrow, int32_t* rows);
+void launch_mg_offsets(hipStream_t stream, int n_mg, int k, const int32_t* box_off,
+                       const int64_t* coff, int64_t* mg_off);
+
+}  // namespace rgc

@@ -1,0 +1,948 @@
+// rgc_kernels.hip — gfx950 kernels for the batched `get_cliques` hot path.
+//
+// One launch of each kernel covers a whole batch of micrographs (SoA/CSR layout in HBM,
+// see DESIGN.md §3).  Reference functions replaced (reference repic/commands/get_cliques.py):
+//   k1_bin            spatial grid (cell >= box_size) so the O(n_a*n_b) pair loop (:59-69)
+//                     becomes a 3x3 cell stencil
+//   k2_pairs<FILL>    calc_jaccard (:40-46) + |dx| <= B prefilter + JI > 0.3 (:64-65,:138),
+//                     two-phase count -> scan -> fill; forward CSR sorted by target box
+//   k4_*              nx.connected_components stats (:145-149), --get_cc (:151-156)
+//   k5_cliques<K,..>  find_cliques (:49-56) as one-box-per-picker k-tuple enumeration by
+//                     sorted neighbour-list intersection, fused with the ILP epilogue
+//                     (:169-190): conf, w, weighted degree, consensus with the CPython
+//                     set-order tie-break (pyset.h)
+//   k7_rank/k7_rows   row index v.index() (:164,:193) as a per-micrograph rank by
+//                     (x, y, id); COO rows (:192-202)
+//
+// Floating point: every JI / degree / median operation keeps the reference's f64 operation
+// order; contraction into FMA is forbidden (the pragma below + -ffp-contract=off).
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "pyset.h"
+#include "rgc_kernels.h"
+
+namespace rgc {
+
+constexpr int WG = 256;
+constexpr int NW = WG / 64;
+
+// ----------------------------------------------------------------------------- helpers
+template <typename T>
+__device__ __forceinline__ T wave_min(T v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ double block_min(double v, double* lds) {
+  v = wave_min(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double r = lds[0];
+  for (int i = 1; i < NW; ++i) r = fmin(r, lds[i]);
+  return r;
+}
+__device__ __forceinline__ double block_max(double v, double* lds) {
+  v = wave_max(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double r = lds[0];
+  for (int i = 1; i < NW; ++i) r = fmax(r, lds[i]);
+  return r;
+}
+
+__device__ __forceinline__ int64_t block_sum64(int64_t v, int64_t* lds) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
+  __syncthreads();
+  int64_t r = 0;
+  for (int i = 0; i < NW; ++i) r += lds[i];
+  return r;
+}
+__device__ __forceinline__ int block_max_i(int v, int* lds) {
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
+  __syncthreads();
+  int r = lds[0];
+  for (int i = 1; i < NW; ++i) r = max(r, lds[i]);
+  return r;
+}
+
+// Exclusive scan of one value per thread across the workgroup.
+__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* lds, int64_t* total) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t inc = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    int64_t t = __shfl_up(inc, o, 64);
+    if (l >= o) inc += t;
+  }
+  __syncthreads();
+  if (l == 63) lds[w] = inc;
+  __syncthreads();
+  int64_t pre = 0, tot = 0;
+  for (int i = 0; i < NW; ++i) {
+    if (i < w) pre += lds[i];
+    tot += lds[i];
+  }
+  *total = tot;
+  return pre + inc - v;
+}
+
+// reference calc_jaccard (get_cliques.py:40-46), same f64 op order, no FMA.
+__device__ __forceinline__ double jaccard(double x, double y, double a, double b, double B,
+                                          double two_b2) {
+  const double xo = fmax((fmin(x, a) + B) - fmax(x, a), 0.0);
+  const double yo = fmax((fmin(y, b) + B) - fmax(y, b), 0.0);
+  const double inter = xo * yo;
+  return inter / (two_b2 - inter);
+}
+
+__device__ __forceinline__ int cell_of(const MgGrid& G, double x, double y) {
+  if (G.ncell == 0 || !isfinite(x) || !isfinite(y)) return G.ncell;  // overflow bucket
+  int cx = (int)fmin(floor((x - G.minx) / G.cell), (double)(G.gx - 1));
+  int cy = (int)fmin(floor((y - G.miny) / G.cell), (double)(G.gy - 1));
+  return cy * G.gx + cx;
+}
+
+// ----------------------------------------------------------------------------- K1 bin
+// One workgroup per micrograph: bounding box, grid choice (cell = box_size, doubled until
+// the grid fits the micrograph's cell budget), LDS counting sort of its boxes by cell.
+__global__ __launch_bounds__(WG) void k1_bin(int k, double B, const int32_t* __restrict__ box_off,
+                                             const int32_t* __restrict__ cell_off,
+                                             const double* __restrict__ x,
+                                             const double* __restrict__ y, MgGrid* grid,
+                                             int32_t* cell_start, double* sx, double* sy,
+                                             int32_t* sbox, uint8_t* spick, int32_t* smg,
+                                             int32_t* bmg, uint8_t* bpick) {
+  __shared__ int32_t cnt[CELL_CAP];
+  __shared__ double redd[NW];
+  __shared__ int64_t red64[NW];
+  __shared__ int32_t poff[MAX_K + 1];
+  __shared__ MgGrid G;
+  const int m = blockIdx.x;
+  const int b0 = box_off[m * k], b1 = box_off[m * k + k], n = b1 - b0;
+  if ((int)threadIdx.x <= k) poff[threadIdx.x] = box_off[m * k + threadIdx.x];
+  double mnx = INFINITY, mny = INFINITY, mxx = -INFINITY, mxy = -INFINITY;
+  for (int i = threadIdx.x; i < n; i += WG) {
+    const double xv = x[b0 + i], yv = y[b0 + i];
+    if (isfinite(xv) && isfinite(yv)) {
+      mnx = fmin(mnx, xv); mxx = fmax(mxx, xv);
+      mny = fmin(mny, yv); mxy = fmax(mxy, yv);
+    }
+  }
+  mnx = block_min(mnx, redd);
+  mny = block_min(mny, redd);
+  mxx = block_max(mxx, redd);
+  mxy = block_max(mxy, redd);
+  if (threadIdx.x == 0) {
+    MgGrid g;
+    g.minx = mnx; g.miny = mny; g.cell = B; g.gx = 0; g.gy = 0; g.ncell = 0; g.pad = 0;
+    const int budget = min(n + 1, CELL_CAP - 1);
+    if (mnx <= mxx && B > 0.0) {
+      const double ex = mxx - mnx, ey = mxy - mny;
+      if (!(ex < 0x1p40 && ey < 0x1p40)) {
+        // coordinates beyond the exactness range of the stencil argument: one cell, all pairs
+        g.cell = INFINITY; g.gx = 1; g.gy = 1;
+      } else {
+        double c = B;
+        for (;;) {
+          const double fx = floor(ex / c) + 1.0, fy = floor(ey / c) + 1.0;
+          if (fx * fy <= (double)budget) { g.gx = (int)fx; g.gy = (int)fy; break; }
+          c *= 2.0;
+        }
+        g.cell = c;
+      }
+      g.ncell = g.gx * g.gy;
+    }
+    G = g;
+    grid[m] = g;
+  }
+  __syncthreads();
+  const int nc = G.ncell;
+  for (int c = threadIdx.x; c <= nc; c += WG) cnt[c] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += WG) atomicAdd(&cnt[cell_of(G, x[b0 + i], y[b0 + i])], 1);
+  __syncthreads();
+  // exclusive scan of cnt[0..nc]
+  const int per = (nc + 1 + WG - 1) / WG;
+  const int c0 = min((int)threadIdx.x * per, nc + 1), c1 = min(c0 + per, nc + 1);
+  int64_t s = 0;
+  for (int c = c0; c < c1; ++c) s += cnt[c];
+  int64_t tot;
+  int64_t pre = block_excl_scan(s, red64, &tot);
+  int32_t* cs = cell_start + cell_off[m];
+  for (int c = c0; c < c1; ++c) {
+    const int v = cnt[c];
+    cnt[c] = (int)pre;
+    cs[c] = (int)pre;
+    pre += v;
+  }
+  if (threadIdx.x == 0) cs[nc + 1] = n;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += WG) {
+    const int g = b0 + i;
+    const double xv = x[g], yv = y[g];
+    int p = 0;
+    while (p + 1 < k && g >= poff[p + 1]) ++p;
+    const int pos = b0 + atomicAdd(&cnt[cell_of(G, xv, yv)], 1);
+    sx[pos] = xv; sy[pos] = yv; sbox[pos] = g; spick[pos] = (uint8_t)p; smg[pos] = m;
+    bmg[g] = m; bpick[g] = (uint8_t)p;
+  }
+}
+
+// ----------------------------------------------------------------------------- K2 pairs
+// One thread per box (in cell order, so neighbouring threads share stencil cells in L1/L2).
+// COUNT: forward-edge count per box.  FILL: write (target, JI) into the box's CSR slot and
+// sort it by target box index (picker-major, file order) for the clique intersections.
+template <bool FILL>
+__global__ __launch_bounds__(WG) void k2_pairs(int N, int k, double B, double two_b2,
+                                               const int32_t* __restrict__ box_off,
+                                               const int32_t* __restrict__ cell_off,
+                                               const MgGrid* __restrict__ grid,
+                                               const int32_t* __restrict__ cell_start,
+                                               const double* __restrict__ sx,
+                                               const double* __restrict__ sy,
+                                               const int32_t* __restrict__ sbox,
+                                               const uint8_t* __restrict__ spick,
+                                               const int32_t* __restrict__ smg, int32_t* fwd_cnt,
+                                               const int64_t* __restrict__ fwd_off,
+                                               int32_t* e_dst, double* e_ji) {
+  const int t = blockIdx.x * WG + threadIdx.x;
+  if (t >= N) return;
+  const int m = smg[t];
+  const MgGrid G = grid[m];
+  const double xa = sx[t], ya = sy[t];
+  const int p = spick[t];
+  const int g = sbox[t];
+  int cnt = 0;
+  int64_t base = 0;
+  if (FILL) base = fwd_off[g];
+  const int c = cell_of(G, xa, ya);
+  if (c < G.ncell) {
+    const int cx = c % G.gx, cy = c / G.gx;
+    const int b0 = box_off[m * k];
+    const int32_t* cs = cell_start + cell_off[m];
+    const int xl = max(cx - 1, 0), xh = min(cx + 1, G.gx - 1);
+    for (int yy = max(cy - 1, 0); yy <= min(cy + 1, G.gy - 1); ++yy) {
+      const int lo = b0 + cs[yy * G.gx + xl], hi = b0 + cs[yy * G.gx + xh + 1];
+      for (int u = lo; u < hi; ++u) {
+        if (spick[u] <= p) continue;
+        const double xb = sx[u];
+        if (!(fabs(xa - xb) <= B)) continue;   // get_cliques.py:64
+        const double ji = jaccard(xa, ya, xb, sy[u], B, two_b2);
+        if (ji > 0.3) {                        // get_cliques.py:65 (threshold :138)
+          if (FILL) { e_dst[base + cnt] = sbox[u]; e_ji[base + cnt] = ji; }
+          ++cnt;
+        }
+      }
+    }
+  }
+  if (!FILL) {
+    fwd_cnt[g] = cnt;
+  } else {
+    for (int i = 1; i < cnt; ++i) {
+      const int kd = e_dst[base + i];
+      const double kj = e_ji[base + i];
+      int j = i - 1;
+      while (j >= 0 && e_dst[base + j] > kd) {
+        e_dst[base + j + 1] = e_dst[base + j];
+        e_ji[base + j + 1] = e_ji[base + j];
+        --j;
+      }
+      e_dst[base + j + 1] = kd;
+      e_ji[base + j + 1] = kj;
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- scan
+// Exclusive scan of int32 counts into int64 offsets (out[n] = total), three launches.
+__global__ __launch_bounds__(WG) void scan_tiles(int64_t n, const int32_t* __restrict__ in,
+                                                 int64_t* tile_sum) {
+  __shared__ int64_t red[NW];
+  const int64_t t0 = (int64_t)blockIdx.x * SCAN_TILE;
+  int64_t s = 0;
+  for (int i = threadIdx.x; i < SCAN_TILE; i += WG) {
+    const int64_t j = t0 + i;
+    if (j < n) s += in[j];
+  }
+  s = block_sum64(s, red);
+  if (threadIdx.x == 0) tile_sum[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(1024) void scan_sums(int64_t nt, int64_t* tile_sum, int64_t* total) {
+  __shared__ int64_t lds[16];
+  __shared__ int64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int64_t b = 0; b < nt; b += 1024) {
+    const int64_t j = b + threadIdx.x;
+    const int64_t v = j < nt ? tile_sum[j] : 0;
+    const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int64_t inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      int64_t t = __shfl_up(inc, o, 64);
+      if (l >= o) inc += t;
+    }
+    if (l == 63) lds[w] = inc;
+    __syncthreads();
+    int64_t pre = 0, tot = 0;
+    for (int i = 0; i < 16; ++i) {
+      if (i < w) pre += lds[i];
+      tot += lds[i];
+    }
+    const int64_t c = carry;
+    if (j < nt) tile_sum[j] = c + pre + inc - v;
+    __syncthreads();
+    if (threadIdx.x == 0) carry = c + tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+__global__ __launch_bounds__(WG) void scan_apply(int64_t n, const int32_t* __restrict__ in,
+                                                 const int64_t* __restrict__ tile_off,
+                                                 const int64_t* __restrict__ total,
+                                                 int64_t* out) {
+  __shared__ int64_t red[NW];
+  constexpr int PER = SCAN_TILE / WG;
+  const int64_t t0 = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * PER;
+  int32_t v[PER];
+  int64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    v[i] = (t0 + i < n) ? in[t0 + i] : 0;
+    s += v[i];
+  }
+  int64_t tot;
+  int64_t pre = block_excl_scan(s, red, &tot) + tile_off[blockIdx.x];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    if (t0 + i < n) out[t0 + i] = pre;
+    pre += v[i];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = *total;
+}
+
+// ----------------------------------------------------------------------------- K4 CC
+__device__ __forceinline__ int ld_par(int32_t* parent, int i) {
+  return __hip_atomic_load(parent + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int uf_find(int32_t* parent, int x) {
+  for (;;) {
+    const int p = ld_par(parent, x);
+    if (p == x) return x;
+    const int gp = ld_par(parent, p);
+    if (gp != p) __hip_atomic_store(parent + x, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    x = gp;
+  }
+}
+
+__global__ __launch_bounds__(WG) void k4_init(int N, int32_t* parent) {
+  const int g = blockIdx.x * WG + threadIdx.x;
+  if (g < N) parent[g] = g;
+}
+
+// Lock-free union-find over the forward edges (hook the larger root under the smaller).
+__global__ __launch_bounds__(WG) void k4_union(int N, const int64_t* __restrict__ fwd_off,
+                                               const int32_t* __restrict__ e_dst, int32_t* parent,
+                                               uint8_t* has_edge) {
+  const int g = blockIdx.x * WG + threadIdx.x;
+  if (g >= N) return;
+  const int64_t e0 = fwd_off[g], e1 = fwd_off[g + 1];
+  if (e0 == e1) return;
+  has_edge[g] = 1;
+  for (int64_t e = e0; e < e1; ++e) {
+    const int h = e_dst[e];
+    has_edge[h] = 1;
+    int a = g, b = h;
+    for (;;) {
+      a = uf_find(parent, a);
+      b = uf_find(parent, b);
+      if (a == b) break;
+      if (a < b) { const int t = a; a = b; b = t; }
+      int expect = a;
+      if (__hip_atomic_compare_exchange_strong(parent + a, &expect, b, __ATOMIC_RELAXED,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        break;
+    }
+  }
+}
+
+__global__ __launch_bounds__(WG) void k4_compress(int N, const uint8_t* __restrict__ has_edge,
+                                                  int32_t* parent, int32_t* csize) {
+  const int g = blockIdx.x * WG + threadIdx.x;
+  if (g >= N || !has_edge[g]) return;
+  const int r = uf_find(parent, g);
+  __hip_atomic_store(parent + g, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  atomicAdd(&csize[r], 1);
+}
+
+// Per-micrograph CC statistics (runtime.tsv columns 2-3) and NO_EDGES status.
+__global__ __launch_bounds__(WG) void k4_stats(int k, const int32_t* __restrict__ box_off,
+                                               const int64_t* __restrict__ fwd_off,
+                                               const uint8_t* __restrict__ has_edge,
+                                               const int32_t* __restrict__ parent,
+                                               const int32_t* __restrict__ csize, MgStat* st) {
+  __shared__ int64_t red[NW];
+  __shared__ int redi[NW];
+  const int m = blockIdx.x;
+  const int b0 = box_off[m * k], b1 = box_off[m * k + k];
+  int64_t nodes = 0, roots = 0;
+  int mx = 0;
+  for (int g = b0 + threadIdx.x; g < b1; g += WG) {
+    if (has_edge[g]) {
+      ++nodes;
+      if (parent[g] == g) { ++roots; mx = max(mx, csize[g]); }
+    }
+  }
+  nodes = block_sum64(nodes, red);
+  roots = block_sum64(roots, red);
+  mx = block_max_i(mx, redi);
+  if (threadIdx.x == 0) {
+    MgStat s;
+    s.n_edges = fwd_off[b1] - fwd_off[b0];
+    s.n_nodes = (int)nodes;
+    s.cc_cnt = (int)roots;
+    s.cc_max = mx;
+    s.status = s.n_edges == 0 ? 1 : 0;
+    s.target = -1;
+    s.n_vert = 0;
+    st[m] = s;
+  }
+}
+
+__device__ __forceinline__ int pair_index(int j, int l, int k) {  // itertools.combinations
+  return j * (2 * k - j - 1) / 2 + (l - j - 1);
+}
+__device__ __forceinline__ uint64_t ins_pack(int pair, int la, int lb, int side) {
+  return ((uint64_t)pair << 49) | ((uint64_t)la << 25) | ((uint64_t)lb << 1) | (uint64_t)side;
+}
+
+// Graph node insertion order (networkx add_node order, get_cliques.py:33-34): a node's key
+// is its first appearance in the edge enumeration (picker pair, a index, b index, side).
+// Only needed where networkx iterates graph order: |G| <= 2k (FilterAtlas) or --get_cc.
+__global__ __launch_bounds__(WG) void k4_ins_keys(int N, int k, int get_cc,
+                                                  const int32_t* __restrict__ box_off,
+                                                  const int32_t* __restrict__ bmg,
+                                                  const uint8_t* __restrict__ bpick,
+                                                  const int64_t* __restrict__ fwd_off,
+                                                  const int32_t* __restrict__ e_dst,
+                                                  const MgStat* __restrict__ st,
+                                                  unsigned long long* ins_key) {
+  const int g = blockIdx.x * WG + threadIdx.x;
+  if (g >= N) return;
+  const int64_t e0 = fwd_off[g], e1 = fwd_off[g + 1];
+  if (e0 == e1) return;
+  const int m = bmg[g];
+  if (!get_cc && st[m].n_nodes > 2 * k) return;
+  const int pa = bpick[g];
+  const int la = g - box_off[m * k + pa];
+  {
+    const int h = e_dst[e0];
+    const int ph = bpick[h];
+    atomicMin(ins_key + g, ins_pack(pair_index(pa, ph, k), la, h - box_off[m * k + ph], 0));
+  }
+  for (int64_t e = e0; e < e1; ++e) {
+    const int h = e_dst[e];
+    const int ph = bpick[h];
+    atomicMin(ins_key + h, ins_pack(pair_index(pa, ph, k), la, h - box_off[m * k + ph], 1));
+  }
+}
+
+__global__ __launch_bounds__(WG) void k4_comp_min(int N, const uint8_t* __restrict__ has_edge,
+                                                  const int32_t* __restrict__ parent,
+                                                  const unsigned long long* __restrict__ ins_key,
+                                                  unsigned long long* comp_min) {
+  const int g = blockIdx.x * WG + threadIdx.x;
+  if (g >= N || !has_edge[g]) return;
+  atomicMin(comp_min + parent[g], ins_key[g]);
+}
+
+// --get_cc: largest CC, ties -> first discovered (smallest first-inserted node).
+__global__ __launch_bounds__(WG) void k4_target(int k, const int32_t* __restrict__ box_off,
+                                                const uint8_t* __restrict__ has_edge,
+                                                const int32_t* __restrict__ parent,
+                                                const int32_t* __restrict__ csize,
+                                                const unsigned long long* __restrict__ comp_min,
+                                                MgStat* st) {
+  __shared__ unsigned long long best[WG];
+  __shared__ int bestg[WG];
+  const int m = blockIdx.x;
+  const int b0 = box_off[m * k], b1 = box_off[m * k + k];
+  const int cmax = st[m].cc_max;
+  unsigned long long bk = ~0ULL;
+  int bg = -1;
+  for (int g = b0 + threadIdx.x; g < b1; g += WG) {
+    if (has_edge[g] && parent[g] == g && csize[g] == cmax && comp_min[g] < bk) {
+      bk = comp_min[g];
+      bg = g;
+    }
+  }
+  best[threadIdx.x] = bk;
+  bestg[threadIdx.x] = bg;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < WG; ++i)
+      if (best[i] < bk) { bk = best[i]; bg = bestg[i]; }
+    st[m].target = bg;
+  }
+}
+
+// ----------------------------------------------------------------------------- K5 cliques
+struct CliqueArgs {
+  int k;
+  int flags;
+  const int32_t* box_off;
+  const int64_t* id_base;
+  const double* x;
+  const double* y;
+  const double* score;
+  const int32_t* bmg;
+  const uint8_t* bpick;
+  const int64_t* fwd_off;
+  const int32_t* e_dst;
+  const double* e_ji;
+  const int32_t* parent;
+  const MgStat* st;
+  const unsigned long long* ins_key;
+  const int64_t* clique_off;
+  int32_t* ccount;
+  int32_t* members;
+  float* w;
+  float* conf;
+  int32_t* consensus;
+  uint8_t* order;
+  uint8_t* in_clique;
+};
+
+__device__ __forceinline__ int64_t lower_bound(const int32_t* a, int64_t lo, int64_t hi, int v) {
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+template <int K>
+struct Walk {
+  int mem[K];        // chosen box per picker
+  double ji[K][K];   // ji[i][j], i < j
+  int pb[K + 1];     // picker box bounds of this micrograph
+  int64_t count;
+  int64_t out;       // next output clique index (FILL)
+  int m;
+};
+
+template <int K>
+__device__ __forceinline__ double median_of(double* v, int n) {
+  // numpy median (numpy/lib/_function_base_impl.py _median): middle value, or the mean of
+  // the two middle values ((a + b) / 2) for even n; NaN if any NaN.
+  for (int i = 0; i < n; ++i)
+    if (isnan(v[i])) return v[i];
+  for (int i = 1; i < n; ++i) {
+    const double t = v[i];
+    int j = i - 1;
+    while (j >= 0 && v[j] > t) { v[j + 1] = v[j]; --j; }
+    v[j + 1] = t;
+  }
+  if (n & 1) return v[n / 2];
+  return (v[n / 2 - 1] + v[n / 2]) / 2.0;
+}
+
+template <int K>
+__device__ void emit_clique(const CliqueArgs& A, Walk<K>& W) {
+  const int64_t j = W.out++;
+  const int m = W.m;
+  double s[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) s[i] = A.score[W.mem[i]];
+  const double conf = median_of<K>(s, K);
+  constexpr int NE = K * (K - 1) / 2;
+  double ej[NE > 0 ? NE : 1];
+  {
+    int t = 0;
+#pragma unroll
+    for (int a = 0; a < K; ++a)
+#pragma unroll
+      for (int b = a + 1; b < K; ++b) ej[t++] = W.ji[a][b];
+  }
+  const double med = median_of<K>(ej, NE);
+  const float conf32 = (float)conf;
+  const float w32 = (float)((double)conf32 * med);
+  // weighted degree: sum of JIs to the other members in increasing picker order
+  // (networkx DegreeView over adjacency insertion order, naive left-to-right f64 sum)
+  double deg[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    double d = 0.0;
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+      if (q == i) continue;
+      d = d + (q < i ? W.ji[q][i] : W.ji[i][q]);
+    }
+    deg[i] = d;
+  }
+  double dmax = deg[0];
+  int nmax = 1, arg = 0;
+#pragma unroll
+  for (int i = 1; i < K; ++i) {
+    if (deg[i] > dmax) { dmax = deg[i]; nmax = 1; arg = i; }
+    else if (deg[i] == dmax) ++nmax;
+  }
+  const bool multi = (A.flags & 2) != 0;
+  int8_t ord[K];
+  if (nmax > 1 || multi) {
+    if (2 * K < A.st[m].n_nodes) {
+      // CPython set(sorted(clique)) iteration order; insertion order is sorted (x, y, id)
+      int8_t srt[K];
+#pragma unroll
+      for (int i = 0; i < K; ++i) srt[i] = (int8_t)i;
+      for (int i = 1; i < K; ++i) {
+        const int8_t t = srt[i];
+        const double tx = A.x[W.mem[t]], ty = A.y[W.mem[t]];
+        const int tg = W.mem[t];
+        int q = i - 1;
+        while (q >= 0) {
+          const int u = W.mem[srt[q]];
+          const double ux = A.x[u], uy = A.y[u];
+          const bool gt = (ux > tx) || (ux == tx && (uy > ty || (uy == ty && u > tg)));
+          if (!gt) break;
+          srt[q + 1] = srt[q];
+          --q;
+        }
+        srt[q + 1] = t;
+      }
+      uint64_t hs[K];
+      const int64_t idb = A.id_base[m] - (int64_t)A.box_off[m * A.k];
+      for (int i = 0; i < K; ++i) {
+        const int g = W.mem[srt[i]];
+        hs[i] = pyset::hash_node(A.x[g], A.y[g], idb + g);
+      }
+      int8_t so[K];
+      pyset::set_order(hs, K, so);
+      for (int i = 0; i < K; ++i) ord[i] = srt[so[i]];
+    } else {
+      // graph insertion order (FilterAtlas iterates the graph when 2k >= |G|)
+      unsigned long long kk[K];
+      for (int i = 0; i < K; ++i) { kk[i] = A.ins_key[W.mem[i]]; ord[i] = (int8_t)i; }
+      for (int i = 1; i < K; ++i) {
+        const int8_t t = ord[i];
+        int q = i - 1;
+        while (q >= 0 && kk[ord[q]] > kk[t]) { ord[q + 1] = ord[q]; --q; }
+        ord[q + 1] = t;
+      }
+    }
+    if (nmax > 1) {
+      for (int i = 0; i < K; ++i)
+        if (deg[ord[i]] == dmax) { arg = ord[i]; break; }
+    }
+  }
+  A.w[j] = w32;
+  A.conf[j] = conf32;
+  A.consensus[j] = W.mem[arg];
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    A.members[j * K + i] = W.mem[i];
+    A.in_clique[W.mem[i]] = 1;
+  }
+  if (multi) {
+    for (int i = 0; i < K; ++i) A.order[j * K + i] = (uint8_t)ord[i];
+  }
+}
+
+// Depth-first enumeration: level D chooses the picker-D member among the forward
+// neighbours of the picker-(D-1) member that are also forward neighbours of every earlier
+// member (sorted-list intersection by binary search).  Static recursion keeps every
+// per-level value in registers.
+template <int K, int D, bool FILL>
+struct Level {
+  __device__ static void run(const CliqueArgs& A, Walk<K>& W) {
+    const int prev = W.mem[D - 1];
+    int64_t lo = A.fwd_off[prev];
+    const int64_t hi0 = A.fwd_off[prev + 1];
+    lo = lower_bound(A.e_dst, lo, hi0, W.pb[D]);
+    const int64_t hi = lower_bound(A.e_dst, lo, hi0, W.pb[D + 1]);
+    for (int64_t e = lo; e < hi; ++e) {
+      const int h = A.e_dst[e];
+      bool ok = true;
+#pragma unroll
+      for (int q = 0; q < D - 1; ++q) {
+        const int c = W.mem[q];
+        const int64_t c0 = A.fwd_off[c], c1 = A.fwd_off[c + 1];
+        const int64_t pos = lower_bound(A.e_dst, c0, c1, h);
+        if (pos >= c1 || A.e_dst[pos] != h) { ok = false; break; }
+        if (FILL) W.ji[q][D] = A.e_ji[pos];
+      }
+      if (!ok) continue;
+      W.mem[D] = h;
+      if (FILL) W.ji[D - 1][D] = A.e_ji[e];
+      Level<K, D + 1, FILL>::run(A, W);
+    }
+  }
+};
+template <int K, bool FILL>
+struct Level<K, K, FILL> {
+  __device__ static void run(const CliqueArgs& A, Walk<K>& W) {
+    if (FILL) emit_clique<K>(A, W);
+    else ++W.count;
+  }
+};
+
+template <int K, bool FILL>
+__global__ __launch_bounds__(WG) void k5_cliques(int N, CliqueArgs A) {
+  const int g = blockIdx.x * WG + threadIdx.x;
+  if (g >= N) return;
+  bool root = A.bpick[g] == 0 && A.fwd_off[g] != A.fwd_off[g + 1];
+  const int m = root ? A.bmg[g] : 0;
+  if (root) {
+    const MgStat s = A.st[m];
+    if (s.status != 0) root = false;
+    if ((A.flags & 1) && A.parent[g] != s.target) root = false;
+  }
+  if (!root) {
+    if (!FILL) A.ccount[g] = 0;
+    return;
+  }
+  Walk<K> W;
+  W.m = m;
+  W.count = 0;
+  W.out = FILL ? A.clique_off[g] : 0;
+#pragma unroll
+  for (int i = 0; i <= K; ++i) W.pb[i] = A.box_off[m * A.k + i];
+  W.mem[0] = g;
+  Level<K, 1, FILL>::run(A, W);
+  if (!FILL) A.ccount[g] = (int32_t)W.count;
+}
+
+// ----------------------------------------------------------------------------- K7 rows
+// Row index of each clique vertex = its rank by (x, y, id) among the micrograph's clique
+// vertices (v = sorted(set(...)); v.index(val), get_cliques.py:164,193).  Bucket the
+// vertices by x (monotone bucket map), then rank inside each bucket by counting.
+__global__ __launch_bounds__(WG) void k7_rank(int k, const int32_t* __restrict__ box_off,
+                                              const double* __restrict__ x,
+                                              const double* __restrict__ y,
+                                              const uint8_t* __restrict__ in_clique,
+                                              int32_t* vlist, int32_t* vsort, int32_t* vrow,
+                                              MgStat* st) {
+  __shared__ int32_t bcnt[RANK_BUCKETS];
+  __shared__ double redd[NW];
+  __shared__ int32_t nv;
+  const int m = blockIdx.x;
+  const int b0 = box_off[m * k], b1 = box_off[m * k + k];
+  if (threadIdx.x == 0) nv = 0;
+  __syncthreads();
+  double mn = INFINITY, mx = -INFINITY;
+  for (int g = b0 + threadIdx.x; g < b1; g += WG) {
+    if (in_clique[g]) {
+      const int pos = atomicAdd(&nv, 1);
+      vlist[b0 + pos] = g;
+      mn = fmin(mn, x[g]);
+      mx = fmax(mx, x[g]);
+    }
+  }
+  mn = block_min(mn, redd);
+  mx = block_max(mx, redd);
+  const int V = nv;
+  if (threadIdx.x == 0) st[m].n_vert = V;
+  if (V == 0) return;
+  const int nb = min(V, RANK_BUCKETS);
+  const double scale = mx > mn ? (double)nb / (mx - mn) : 0.0;
+  for (int b = threadIdx.x; b < nb; b += WG) bcnt[b] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < V; i += WG) {
+    const int g = vlist[b0 + i];
+    const int bk = min(nb - 1, (int)((x[g] - mn) * scale));
+    atomicAdd(&bcnt[bk], 1);
+  }
+  __syncthreads();
+  {  // exclusive scan of bcnt[0..nb)
+    __shared__ int64_t red64[NW];
+    const int per = (nb + WG - 1) / WG;
+    const int c0 = min((int)threadIdx.x * per, nb), c1 = min(c0 + per, nb);
+    int64_t s = 0;
+    for (int c = c0; c < c1; ++c) s += bcnt[c];
+    int64_t tot;
+    int64_t pre = block_excl_scan(s, red64, &tot);
+    for (int c = c0; c < c1; ++c) {
+      const int v = bcnt[c];
+      bcnt[c] = (int)pre;
+      pre += v;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < V; i += WG) {
+    const int g = vlist[b0 + i];
+    const int bk = min(nb - 1, (int)((x[g] - mn) * scale));
+    vsort[b0 + atomicAdd(&bcnt[bk], 1)] = g;
+  }
+  __syncthreads();
+  // after the scatter bcnt[b] = end of bucket b = start of bucket b + 1
+  for (int i = threadIdx.x; i < V; i += WG) {
+    const int g = vlist[b0 + i];
+    const double gx = x[g], gy = y[g];
+    const int bk = min(nb - 1, (int)((gx - mn) * scale));
+    const int lo = bk > 0 ? bcnt[bk - 1] : 0, hi = bcnt[bk];
+    int r = lo;
+    for (int q = lo; q < hi; ++q) {
+      const int u = vsort[b0 + q];
+      const double ux = x[u], uy = y[u];
+      r += (ux < gx) || (ux == gx && (uy < gy || (uy == gy && u < g)));
+    }
+    vrow[g] = r;
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(WG) void k7_rows(int64_t C, const int32_t* __restrict__ members,
+                                              const int32_t* __restrict__ vrow, int32_t* rows) {
+  const int64_t j = (int64_t)blockIdx.x * WG + threadIdx.x;
+  if (j >= C) return;
+  int r[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) r[i] = vrow[members[j * K + i]];
+  for (int i = 1; i < K; ++i) {
+    const int t = r[i];
+    int q = i - 1;
+    while (q >= 0 && r[q] > t) { r[q + 1] = r[q]; --q; }
+    r[q + 1] = t;
+  }
+#pragma unroll
+  for (int i = 0; i < K; ++i) rows[j * K + i] = r[i];
+}
+
+__global__ __launch_bounds__(WG) void k_mg_offsets(int n_mg, int k, const int32_t* __restrict__ box_off,
+                                                   const int64_t* __restrict__ coff,
+                                                   int64_t* mg_off) {
+  const int m = blockIdx.x * WG + threadIdx.x;
+  if (m > n_mg) return;
+  mg_off[m] = coff[box_off[m * k]];
+}
+
+// ----------------------------------------------------------------------------- launchers
+#define RGC_LAUNCH(kern, grid, block, ...) \
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(block), 0, stream, __VA_ARGS__)
+
+void launch_bin(hipStream_t stream, int n_mg, int k, double B, const int32_t* box_off,
+                const int32_t* cell_off, const double* x, const double* y, MgGrid* grid,
+                int32_t* cell_start, double* sx, double* sy, int32_t* sbox, uint8_t* spick,
+                int32_t* smg, int32_t* bmg, uint8_t* bpick) {
+  RGC_LAUNCH(k1_bin, n_mg, WG, k, B, box_off, cell_off, x, y, grid, cell_start, sx, sy, sbox,
+             spick, smg, bmg, bpick);
+}
+
+void launch_pairs(hipStream_t stream, bool fill, int N, int k, double B, double two_b2,
+                  const int32_t* box_off, const int32_t* cell_off, const MgGrid* grid,
+                  const int32_t* cell_start, const double* sx, const double* sy,
+                  const int32_t* sbox, const uint8_t* spick, const int32_t* smg,
+                  int32_t* fwd_cnt, const int64_t* fwd_off, int32_t* e_dst, double* e_ji) {
+  const int nb = (N + WG - 1) / WG;
+  if (nb == 0) return;
+  if (fill)
+    RGC_LAUNCH(k2_pairs<true>, nb, WG, N, k, B, two_b2, box_off, cell_off, grid, cell_start, sx,
+               sy, sbox, spick, smg, fwd_cnt, fwd_off, e_dst, e_ji);
+  else
+    RGC_LAUNCH(k2_pairs<false>, nb, WG, N, k, B, two_b2, box_off, cell_off, grid, cell_start,
+               sx, sy, sbox, spick, smg, fwd_cnt, fwd_off, e_dst, e_ji);
+}
+
+int64_t scan_tiles_needed(int64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 1; }
+
+void launch_scan(hipStream_t stream, int64_t n, const int32_t* in, int64_t* out,
+                 int64_t* tile_buf, int64_t* total) {
+  const int64_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
+  if (nt > 0) RGC_LAUNCH(scan_tiles, nt, WG, n, in, tile_buf);
+  RGC_LAUNCH(scan_sums, 1, 1024, nt, tile_buf, total);
+  if (nt > 0) RGC_LAUNCH(scan_apply, nt, WG, n, in, tile_buf, total, out);
+  else (void)hipMemcpyAsync(out, total, sizeof(int64_t), hipMemcpyDeviceToDevice, stream);
+}
+
+void launch_cc(hipStream_t stream, int phase, int N, int n_mg, int k, int get_cc,
+               const int32_t* box_off, const int32_t* bmg, const uint8_t* bpick,
+               const int64_t* fwd_off, const int32_t* e_dst, int32_t* parent, uint8_t* has_edge,
+               int32_t* csize, MgStat* st, unsigned long long* ins_key,
+               unsigned long long* comp_min) {
+  const int nb = (N + WG - 1) / WG;
+  switch (phase) {
+    case 0: if (nb) RGC_LAUNCH(k4_init, nb, WG, N, parent); break;
+    case 1: if (nb) RGC_LAUNCH(k4_union, nb, WG, N, fwd_off, e_dst, parent, has_edge); break;
+    case 2: if (nb) RGC_LAUNCH(k4_compress, nb, WG, N, has_edge, parent, csize); break;
+    case 3: RGC_LAUNCH(k4_stats, n_mg, WG, k, box_off, fwd_off, has_edge, parent, csize, st); break;
+    case 4:
+      if (nb) RGC_LAUNCH(k4_ins_keys, nb, WG, N, k, get_cc, box_off, bmg, bpick, fwd_off, e_dst,
+                         st, ins_key);
+      break;
+    case 5: if (nb) RGC_LAUNCH(k4_comp_min, nb, WG, N, has_edge, parent, ins_key, comp_min); break;
+    case 6: RGC_LAUNCH(k4_target, n_mg, WG, k, box_off, has_edge, parent, csize, comp_min, st); break;
+  }
+}
+
+template <int K>
+static void launch_cliques_k(hipStream_t stream, bool fill, int N, const CliqueArgsHost& h) {
+  CliqueArgs A;
+  A.k = h.k; A.flags = h.flags; A.box_off = h.box_off; A.id_base = h.id_base; A.x = h.x;
+  A.y = h.y; A.score = h.score; A.bmg = h.bmg; A.bpick = h.bpick; A.fwd_off = h.fwd_off;
+  A.e_dst = h.e_dst; A.e_ji = h.e_ji; A.parent = h.parent; A.st = h.st; A.ins_key = h.ins_key;
+  A.clique_off = h.clique_off; A.ccount = h.ccount; A.members = h.members; A.w = h.w;
+  A.conf = h.conf; A.consensus = h.consensus; A.order = h.order; A.in_clique = h.in_clique;
+  const int nb = (N + WG - 1) / WG;
+  if (!nb) return;
+  if (fill) RGC_LAUNCH((k5_cliques<K, true>), nb, WG, N, A);
+  else RGC_LAUNCH((k5_cliques<K, false>), nb, WG, N, A);
+}
+
+int launch_cliques(hipStream_t stream, bool fill, int N, const CliqueArgsHost& h) {
+  switch (h.k) {
+    case 2: launch_cliques_k<2>(stream, fill, N, h); break;
+    case 3: launch_cliques_k<3>(stream, fill, N, h); break;
+    case 4: launch_cliques_k<4>(stream, fill, N, h); break;
+    case 5: launch_cliques_k<5>(stream, fill, N, h); break;
+    case 6: launch_cliques_k<6>(stream, fill, N, h); break;
+    case 7: launch_cliques_k<7>(stream, fill, N, h); break;
+    case 8: launch_cliques_k<8>(stream, fill, N, h); break;
+    default: return -1;
+  }
+  return 0;
+}
+
+void launch_rank(hipStream_t stream, int n_mg, int k, const int32_t* box_off, const double* x,
+                 const double* y, const uint8_t* in_clique, int32_t* vlist, int32_t* vsort,
+                 int32_t* vrow, MgStat* st) {
+  RGC_LAUNCH(k7_rank, n_mg, WG, k, box_off, x, y, in_clique, vlist, vsort, vrow, st);
+}
+
+int launch_rows(hipStream_t stream, int k, int64_t C, const int32_t* members,
+                const int32_t* vrow, int32_t* rows) {
+  const int64_t nb = (C + WG - 1) / WG;
+  if (!nb) return 0;
+  switch (k) {
+    case 2: RGC_LAUNCH(k7_rows<2>, nb, WG, C, members, vrow, rows); break;
+    case 3: RGC_LAUNCH(k7_rows<3>, nb, WG, C, members, vrow, rows); break;
+    case 4: RGC_LAUNCH(k7_rows<4>, nb, WG, C, members, vrow, rows); break;
+    case 5: RGC_LAUNCH(k7_rows<5>, nb, WG, C, members, vrow, rows); break;
+    case 6: RGC_LAUNCH(k7_rows<6>, nb, WG, C, members, vrow, rows); break;
+    case 7: RGC_LAUNCH(k7_rows<7>, nb, WG, C, members, vrow, rows); break;
+    case 8: RGC_LAUNCH(k7_rows<8>, nb, WG, C, members, vrow, rows); break;
+    default: return -1;
+  }
+  return 0;
+}
+
+void launch_mg_offsets(hipStream_t stream, int n_mg, int k, const int32_t* box_off,
+                       const int64_t* coff, int64_t* mg_off) {
+  RGC_LAUNCH(k_mg_offsets, (n_mg + 1 + WG - 1) / WG, WG, n_mg, k, box_off, coff, mg_off);
+}
+
+}  // namespace rgc

@@ -1,0 +1,221 @@
+"""ctypes binding of ``librepic_gc.so`` (C-ABI declared in ``include/repic_gc.h``).
+
+The library is built in-tree by ``repic-copy_amd/csrc/Makefile`` (``__graft_entry__.build``).
+Importing this module without the built library raises ImportError: there is no CPU
+fallback for the hot path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librepic_gc.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} is missing: build it with `make -C repic-copy_amd/csrc` "
+        "(or __graft_entry__.build()); the get_cliques hot path has no CPU fallback")
+
+lib = C.CDLL(LIB_PATH)
+
+F_GET_CC, F_MULTI_OUT, F_DEVICE_INPUTS, F_HOST_OUTPUTS, F_TIMING = 1, 2, 4, 8, 16
+OK, NO_EDGES, NO_CLIQUES = 0, 1, 2
+PARSE_OK, PARSE_INDEX, PARSE_VALUE, PARSE_ASSERT, PARSE_FALLBACK, PARSE_OSERROR = range(6)
+MAX_K = 8
+
+_i32p = C.POINTER(C.c_int32)
+_i64p = C.POINTER(C.c_int64)
+_f64p = C.POINTER(C.c_double)
+_f32p = C.POINTER(C.c_float)
+_u8p = C.POINTER(C.c_uint8)
+
+
+class BatchIn(C.Structure):
+    _fields_ = [("n_mg", C.c_int32), ("k", C.c_int32), ("box_size", C.c_int64),
+                ("flags", C.c_uint32), ("box_off", _i64p), ("id_base", _i64p),
+                ("x", C.c_void_p), ("y", C.c_void_p), ("score", C.c_void_p)]
+
+
+class BatchOut(C.Structure):
+    _fields_ = [("n_boxes", C.c_int64), ("n_edges", C.c_int64), ("n_cliques", C.c_int64),
+                ("status", _i32p), ("cc_max", _i32p), ("cc_cnt", _i32p), ("n_nodes", _i32p),
+                ("n_vert", _i32p), ("n_edges_mg", _i64p), ("clique_off", _i64p),
+                ("rows", C.c_void_p), ("w", C.c_void_p), ("conf", C.c_void_p),
+                ("consensus", C.c_void_p), ("members", C.c_void_p), ("order", C.c_void_p)]
+
+
+class Parsed(C.Structure):
+    _fields_ = [("n_files", C.c_int64), ("status", _i32p), ("off", _i64p), ("x", _f64p),
+                ("y", _f64p), ("score", _f64p), ("sigmoid", _u8p)]
+
+
+lib.rgc_abi_version.restype = C.c_int
+lib.rgc_last_error.restype = C.c_char_p
+lib.rgc_device_count.argtypes = [C.POINTER(C.c_int)]
+lib.rgc_ctx_create.argtypes = [C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]
+lib.rgc_ctx_destroy.argtypes = [C.c_void_p]
+lib.rgc_ctx_destroy.restype = None
+lib.rgc_run.argtypes = [C.c_void_p, C.POINTER(BatchIn), C.POINTER(BatchOut)]
+lib.rgc_kernel_times.argtypes = [C.c_void_p, C.c_int, _f32p, C.POINTER(C.c_char_p)]
+lib.rgc_parse_files.argtypes = [C.POINTER(C.c_char_p), C.c_int64, C.c_int,
+                                C.POINTER(C.POINTER(Parsed))]
+lib.rgc_parsed_free.argtypes = [C.POINTER(Parsed)]
+lib.rgc_parsed_free.restype = None
+lib.rgc_py_hash_node.argtypes = [C.c_double, C.c_double, C.c_int64]
+lib.rgc_py_hash_node.restype = C.c_uint64
+lib.rgc_py_set_order.argtypes = [C.POINTER(C.c_uint64), C.c_int, C.POINTER(C.c_int8)]
+
+EXPORTS = ["rgc_abi_version", "rgc_last_error", "rgc_device_count", "rgc_ctx_create",
+           "rgc_ctx_destroy", "rgc_run", "rgc_kernel_times", "rgc_parse_files",
+           "rgc_parsed_free", "rgc_py_hash_node", "rgc_py_set_order"]
+
+
+class RGCError(RuntimeError):
+    pass
+
+
+def _check(rc):
+    if rc < 0:
+        raise RGCError(lib.rgc_last_error().decode(errors="replace"))
+    return rc
+
+
+def abi_version() -> int:
+    return lib.rgc_abi_version()
+
+
+# ----------------------------------------------------------------------------- parsing
+def parse_files(paths, n_threads=None):
+    """Parse BOX files with the C++ parser -> (status[n], off[n+1], x, y, score, sigmoid)."""
+    n = len(paths)
+    arr = (C.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
+    out = C.POINTER(Parsed)()
+    if n_threads is None:
+        n_threads = min(16, os.cpu_count() or 1)
+    _check(lib.rgc_parse_files(arr, n, int(n_threads), C.byref(out)))
+    try:
+        P = out.contents
+        status = np.ctypeslib.as_array(P.status, shape=(n,)).copy() if n else np.zeros(0, np.int32)
+        off = np.ctypeslib.as_array(P.off, shape=(n + 1,)).copy()
+        tot = int(off[-1])
+        if tot:
+            x = np.ctypeslib.as_array(P.x, shape=(tot,)).copy()
+            y = np.ctypeslib.as_array(P.y, shape=(tot,)).copy()
+            s = np.ctypeslib.as_array(P.score, shape=(tot,)).copy()
+        else:
+            x = y = s = np.zeros(0, np.float64)
+        sig = (np.ctypeslib.as_array(P.sigmoid, shape=(n,)).astype(bool) if n
+               else np.zeros(0, bool))
+    finally:
+        lib.rgc_parsed_free(out)
+    return status, off, x, y, s, sig
+
+
+# ----------------------------------------------------------------------------- CPython set order
+def py_hash_node(x: float, y: float, node_id: int) -> int:
+    return int(lib.rgc_py_hash_node(x, y, node_id))
+
+
+def py_set_order(hashes):
+    n = len(hashes)
+    h = (C.c_uint64 * max(n, 1))(*[int(v) & 0xFFFFFFFFFFFFFFFF for v in hashes])
+    o = (C.c_int8 * max(n, 1))()
+    _check(lib.rgc_py_set_order(h, n, o))
+    return [o[i] for i in range(n)]
+
+
+# ----------------------------------------------------------------------------- device context
+def device_count() -> int:
+    n = C.c_int(0)
+    _check(lib.rgc_device_count(C.byref(n)))
+    return n.value
+
+
+class Context:
+    """One device + stream; owns the device workspace arena (grow-only)."""
+
+    def __init__(self, device: int = 0, stream: int | None = None):
+        self._p = C.c_void_p()
+        _check(lib.rgc_ctx_create(int(device), C.c_void_p(stream or 0), C.byref(self._p)))
+        self.device = device
+
+    def close(self):
+        if self._p:
+            lib.rgc_ctx_destroy(self._p)
+            self._p = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def run(self, n_mg, k, box_size, box_off, id_base, x, y, score, flags=F_HOST_OUTPUTS):
+        """Run the batched pipeline.  ``box_off``/``id_base`` are host int64 arrays;
+        ``x``/``y``/``score`` are host float64 arrays, or device pointers (ints) with
+        ``F_DEVICE_INPUTS``.  Returns a :class:`Result` (views into context-owned memory
+        that stay valid until the next ``run``)."""
+        box_off = np.ascontiguousarray(box_off, dtype=np.int64)
+        id_base = np.ascontiguousarray(id_base, dtype=np.int64)
+        assert box_off.shape == (n_mg * k + 1,) and id_base.shape == (n_mg,)
+        keep = [box_off, id_base]
+        if flags & F_DEVICE_INPUTS:
+            px, py, ps = (C.c_void_p(int(v)) for v in (x, y, score))
+        else:
+            x, y, score = (np.ascontiguousarray(v, dtype=np.float64) for v in (x, y, score))
+            n = int(box_off[-1]) if len(box_off) else 0
+            assert x.shape == y.shape == score.shape == (n,)
+            keep += [x, y, score]
+            px, py, ps = (C.c_void_p(v.ctypes.data) for v in (x, y, score))
+        bi = BatchIn(n_mg, k, int(box_size), flags, box_off.ctypes.data_as(_i64p),
+                     id_base.ctypes.data_as(_i64p), px, py, ps)
+        bo = BatchOut()
+        _check(lib.rgc_run(self._p, C.byref(bi), C.byref(bo)))
+        del keep
+        return Result(bo, n_mg, k, flags)
+
+    def kernel_times(self):
+        n = lib.rgc_kernel_times(self._p, 0, None, None)
+        ms = (C.c_float * max(n, 1))()
+        names = (C.c_char_p * max(n, 1))()
+        lib.rgc_kernel_times(self._p, n, ms, names)
+        return [(names[i].decode(), float(ms[i])) for i in range(n)]
+
+
+class Result:
+    """Host view of one rgc_run.  Per-clique arrays are numpy views of pinned host memory
+    (F_HOST_OUTPUTS) or raw device pointers otherwise."""
+
+    def __init__(self, bo: BatchOut, n_mg: int, k: int, flags: int):
+        self.n_mg, self.k = n_mg, k
+        self.n_boxes, self.n_edges, self.n_cliques = bo.n_boxes, bo.n_edges, bo.n_cliques
+
+        def a(p, n):
+            return np.ctypeslib.as_array(p, shape=(n,)).copy() if n else np.zeros(0)
+
+        self.status = a(bo.status, n_mg).astype(np.int32)
+        self.cc_max = a(bo.cc_max, n_mg).astype(np.int32)
+        self.cc_cnt = a(bo.cc_cnt, n_mg).astype(np.int32)
+        self.n_nodes = a(bo.n_nodes, n_mg).astype(np.int32)
+        self.n_vert = a(bo.n_vert, n_mg).astype(np.int32)
+        self.n_edges_mg = a(bo.n_edges_mg, n_mg).astype(np.int64)
+        self.clique_off = a(bo.clique_off, n_mg + 1).astype(np.int64)
+        C_ = int(self.n_cliques)
+        if flags & F_HOST_OUTPUTS:
+            def h(p, ct, n):
+                if not n or not p:
+                    return np.zeros(n, dtype=np.dtype(ct))
+                return np.ctypeslib.as_array(C.cast(p, C.POINTER(ct)), shape=(n,))
+            self.rows = h(bo.rows, C.c_int32, C_ * k).reshape(C_, k)
+            self.w = h(bo.w, C.c_float, C_)
+            self.conf = h(bo.conf, C.c_float, C_)
+            self.consensus = h(bo.consensus, C.c_int32, C_)
+            self.members = h(bo.members, C.c_int32, C_ * k).reshape(C_, k)
+            self.order = (h(bo.order, C.c_uint8, C_ * k).reshape(C_, k)
+                          if (flags & F_MULTI_OUT) else None)
+        else:
+            self.rows, self.w, self.conf = bo.rows, bo.w, bo.conf
+            self.consensus, self.members, self.order = bo.consensus, bo.members, bo.order

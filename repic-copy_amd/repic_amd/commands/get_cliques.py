@@ -1,0 +1,125 @@
+"""``repic get_cliques`` — drop-in subcommand, MI355X hot path.
+
+Same plugin protocol as the reference module (reference repic/commands/get_cliques.py:13-27,72):
+``name``, ``add_arguments(parser)``, ``main(args)``; same positional arguments and flags;
+same side effects (``out_dir`` deleted and recreated, the same five files per micrograph,
+an empty ``<base>.box`` for skipped micrographs) and the same exception classes at the same
+micrograph when the reference would crash.  The work between parsing and writing runs as
+batched HIP kernels (``librepic_gc.so``); there is no CPU fallback.
+
+Extra options (do not change outputs): ``--batch_boxes`` (boxes per device batch),
+``--threads`` (host parser threads), ``--device``.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+from .. import _lib
+from ..ingest import DirIndex, list_methods, plan, probe_start_method
+from ..pipeline import Batch, run_batch, split_batches
+from ..writers import (consensus_coords, constraint_matrix, multi_out_coords, write_micrograph,
+                       write_skip)
+
+name = "get_cliques"
+
+
+def add_arguments(parser):
+    """Same CLI surface as the reference (get_cliques.py:16-27) plus tuning knobs."""
+    parser.add_argument("in_dir",
+                        help="path to input directory containing subdirectories of particle coordinate files ")
+    parser.add_argument("out_dir",
+                        help="path to output directory (WARNING - script will delete directory if it exists)")
+    parser.add_argument("box_size", type=int,
+                        help="particle detection box size (in int[pixels])")
+    parser.add_argument("--multi_out", action="store_true",
+                        help="set output of cliques to be members sorted by picker name")
+    parser.add_argument("--get_cc", action="store_true",
+                        help="filters cliques for those in the largest Connected Component (CC)")
+    parser.add_argument("--batch_boxes", type=int, default=1 << 25,
+                        help="max boxes per device batch (does not change outputs)")
+    parser.add_argument("--threads", type=int, default=None,
+                        help="host BOX-parser threads (does not change outputs)")
+    parser.add_argument("--device", type=int, default=None,
+                        help="HIP device (default: $LOCAL_RANK or 0)")
+
+
+def _del_dir(path):
+    p = Path(path)
+    if p.exists() and p.is_dir():
+        shutil.rmtree(p)
+
+
+def main(args):
+    assert os.path.exists(args.in_dir), "Error - input directory does not exist"
+    _del_dir(args.out_dir)
+    methods = list_methods(args.in_dir)
+    Path(args.out_dir).mkdir(parents=True, exist_ok=True)
+    listing = getattr(args, "listing", None)     # tests: replay a recorded readdir order
+    index = DirIndex(args.in_dir, methods, listing)
+    start = probe_start_method(index, methods)
+    print(f"Using {start} BOX files as starting point")
+    t_plan = time.time()
+    mgs, crash = plan(args.in_dir, methods, index, n_threads=getattr(args, "threads", None))
+    k = len(methods)
+    ok = [mg for mg in mgs if mg.status == "ok"]
+    t_plan = time.time() - t_plan
+    results = {}
+    t_dev = 0.0
+    if ok:
+        dev = args.device if getattr(args, "device", None) is not None else int(
+            os.environ.get("LOCAL_RANK", "0"))
+        ctx = _lib.Context(dev)
+        counts = [sum(c.n for c in mg.coords) for mg in ok]
+        for m0, m1 in split_batches(counts, getattr(args, "batch_boxes", 1 << 25)):
+            part = ok[m0:m1]
+            batch = Batch.pack(k, args.box_size, [[(c.x, c.y, c.s) for c in mg.coords]
+                                                 for mg in part],
+                               id_bases=[mg.id_base for mg in part])
+            t0 = time.time()
+            res = run_batch(ctx, batch, get_cc=args.get_cc, multi_out=args.multi_out)
+            t_dev += time.time() - t0
+            for j, mg in enumerate(part):
+                results[id(mg)] = (batch, j, res[j])
+        ctx.close()
+    share = (t_plan + t_dev) / max(1, len(mgs))
+    for mg in mgs:
+        print(f"\n--- {mg.base} ---\n")
+        if mg.status == "skip":
+            print("Skipping micrograph - not all methods have picked particles...")
+            write_skip(args.out_dir, mg.base)
+            continue
+        if mg.status == "crash":
+            raise mg.exc
+        t0 = time.time()
+        batch, j, r = results[id(mg)]
+        if r.status == _lib.NO_EDGES:
+            raise ValueError("zero-size array to reduction operation maximum which has no identity")
+        if r.status == _lib.NO_CLIQUES:
+            raise UnboundLocalError("local variable 'clique' referenced before assignment")
+        b0 = int(batch.box_off[j * k])
+        idb = int(batch.id_base[j]) - b0
+        if args.multi_out:
+            def tup(g):
+                return (float(batch.x[g]), float(batch.y[g]), idb + int(g))
+            member_tuples = [[tup(g) for g in row] for row in r.members.tolist()]
+            picker_coords = []
+            for p, c in enumerate(mg.coords):
+                ids = range(idb + int(batch.box_off[j * k + p]),
+                            idb + int(batch.box_off[j * k + p + 1]))
+                ws = list(c.s) if c.sigmoid else c.s.tolist()
+                picker_coords.append(list(zip(c.x.tolist(), c.y.tolist(), ws, ids)))
+            coords = multi_out_coords(methods, member_tuples, r.order.tolist(), k, args.get_cc,
+                                      picker_coords)
+        else:
+            g = r.consensus.astype(np.int64)
+            coords = consensus_coords(batch.x[g], batch.y[g], idb + g)
+        A = constraint_matrix(r.rows, r.n_vert)
+        write_micrograph(args.out_dir, mg.base, r.w, coords, r.conf, A,
+                         share + (time.time() - t0), r.cc_max, r.cc_cnt)
+    sys.stdout.flush()

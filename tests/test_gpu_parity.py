@@ -1,0 +1,144 @@
+"""GPU parity: the HIP path (through the C-ABI) against the reference's golden outputs and the
+CPU oracle.  Bit-exact: clique sets, constraint matrices, float32 weights / confidences,
+consensus coordinates (canonical column order); f64 Jaccard indices enter
+only through those outputs, so the 1e-12 relative tolerance of BASELINE.json is met with 0.
+"""
+import argparse
+import builtins
+import os
+
+import numpy as np
+import pytest
+
+from golden_util import assert_matches_golden, golden_cases, load_case, make_inputs, read_outputs
+
+pytestmark = pytest.mark.gpu
+
+
+def _args(in_dir, out_dir, meta, **kw):
+    a = argparse.Namespace(in_dir=in_dir, out_dir=out_dir, box_size=meta["box"],
+                           multi_out="--multi_out" in meta["flags"],
+                           get_cc="--get_cc" in meta["flags"], batch_boxes=1 << 25,
+                           threads=None, device=None, listing=meta["listing"])
+    for k_, v in kw.items():
+        setattr(a, k_, v)
+    return a
+
+
+def _run_case(name, tmp_path, **kw):
+    from repic_amd.commands import get_cliques
+    meta, data = load_case(name)
+    in_dir = make_inputs(name, str(tmp_path))
+    out_dir = os.path.join(str(tmp_path), "out")
+    exc = None
+    try:
+        get_cliques.main(_args(in_dir, out_dir, meta, **kw))
+    except Exception as e:  # noqa: BLE001 - the exception class is part of the contract
+        exc = e
+    if meta["exception"]:
+        assert exc is not None and isinstance(exc, getattr(builtins, meta["exception"])), exc
+    else:
+        assert exc is None, repr(exc)
+    mgs, arrays = read_outputs(out_dir, meta)
+    assert_matches_golden(meta, data, mgs, arrays)
+
+
+@pytest.mark.parametrize("name", golden_cases())
+def test_gpu_matches_reference_golden(name, tmp_path):
+    _run_case(name, tmp_path)
+
+
+@pytest.mark.parametrize("name", ["c1_10017", "syn_k3", "skips", "ties_getcc"])
+def test_gpu_multi_batch_split(name, tmp_path):
+    """Splitting the micrographs over several device batches changes nothing."""
+    _run_case(name, tmp_path, batch_boxes=2000)
+
+
+# ----------------------------------------------------------------------------- vs oracle
+def _oracle_mg(mg, box, methods, id_base, get_cc=False):
+    from oracle import cpu_ref
+    coords, nid = [], id_base
+    for (x, y, s) in mg:
+        coords.append([(float(a), float(b), float(c), nid + i)
+                       for i, (a, b, c) in enumerate(zip(x, y, s))])
+        nid += len(x)
+    return cpu_ref.micrograph(coords, box, methods, get_cc=get_cc)
+
+
+def _canon(rows, w, conf, cons_xyid):
+    perm = np.lexsort(np.asarray(rows).T[::-1]) if len(rows) else np.zeros(0, int)
+    return (np.asarray(rows)[perm], np.asarray(w)[perm].view(np.uint32),
+            np.asarray(conf)[perm].view(np.uint32), [cons_xyid[i] for i in perm])
+
+
+@pytest.mark.parametrize("cfg_name,n_mg,get_cc", [("C2", 24, False), ("C2", 8, True),
+                                                   ("C4", 6, False)])
+def test_gpu_matches_oracle_synthetic(cfg_name, n_mg, get_cc):
+    from repic_amd import _lib, synth
+    from repic_amd.pipeline import Batch, run_batch
+    cfg = synth.SynthConfig(**synth.CONFIGS[cfg_name], seed=5, logit=(1,))
+    mgs = synth.batch(cfg, n_mg)
+    from repic_amd.ingest import sigmoid
+    mgs = [[(x, y, sigmoid(s) if s.min() < 0 else s) for (x, y, s) in mg] for mg in mgs]
+    batch = Batch.pack(cfg.k, cfg.box, mgs)
+    ctx = _lib.Context(0)
+    res = run_batch(ctx, batch, get_cc=get_cc)
+    methods = [f"picker{p}" for p in range(cfg.k)]
+    for m, mg in enumerate(mgs):
+        o = _oracle_mg(mg, cfg.box, methods, int(batch.id_base[m]), get_cc)
+        r = res[m]
+        assert r.status == _lib.OK
+        assert (r.cc_max, r.cc_cnt) == (o["cc_max"], o["cc_cnt"])
+        A = o["A"].tocoo()
+        C = A.shape[1]
+        orows = np.sort(A.row[np.argsort(A.col, kind="stable")].reshape(C, cfg.k), axis=1)
+        assert r.n_vert == A.shape[0] and len(r.w) == C
+        b0 = int(batch.box_off[m * cfg.k])
+        idb = int(batch.id_base[m]) - b0
+        gcons = [(float(batch.x[g]), float(batch.y[g]), idb + int(g)) for g in r.consensus]
+        a = _canon(orows, o["w"], o["conf"], o["consensus"])
+        b = _canon(r.rows, r.w, r.conf, gcons)
+        assert np.array_equal(a[0], b[0])
+        assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+        assert a[3] == b[3]
+    ctx.close()
+
+
+def test_gpu_full_c2_properties():
+    """Full BASELINE config #2 (10k micrographs): size-independent invariants."""
+    from repic_amd import _lib, synth
+    from repic_amd.pipeline import Batch
+    cfg = synth.SynthConfig(**synth.CONFIGS["C2"], seed=0)
+    batch = Batch.pack(cfg.k, cfg.box, synth.batch(cfg, 10000))
+    ctx = _lib.Context(0)
+    r = ctx.run(batch.n_mg, cfg.k, cfg.box, batch.box_off, batch.id_base, batch.x, batch.y,
+                batch.score, _lib.F_HOST_OUTPUTS)
+    assert (r.status == 0).all()
+    C = int(r.n_cliques)
+    assert C == int(r.clique_off[-1]) and C > 10000 * 300
+    mem = r.members.astype(np.int64)
+    # members: one box per picker, inside their micrograph
+    mg_of = np.searchsorted(batch.box_off[::cfg.k], mem[:, 0], side="right") - 1
+    for p in range(cfg.k):
+        lo = batch.box_off[mg_of * cfg.k + p]
+        hi = batch.box_off[mg_of * cfg.k + p + 1]
+        assert ((mem[:, p] >= lo) & (mem[:, p] < hi)).all()
+    # every pair of members overlaps with JI > 0.3 (f64, reference op order)
+    B = float(cfg.box)
+    for a in range(cfg.k):
+        for b in range(a + 1, cfg.k):
+            xa, ya, xb, yb = batch.x[mem[:, a]], batch.y[mem[:, a]], batch.x[mem[:, b]], batch.y[mem[:, b]]
+            xo = np.maximum((np.minimum(xa, xb) + B) - np.maximum(xa, xb), 0.0)
+            yo = np.maximum((np.minimum(ya, yb) + B) - np.maximum(ya, yb), 0.0)
+            inter = xo * yo
+            assert (inter / (2 * B * B - inter) > 0.3).all()
+    # rows ascending and within [0, V)
+    rows = r.rows
+    assert (np.diff(rows, axis=1) > 0).all()
+    vm = r.n_vert[mg_of]
+    assert (rows[:, -1] < vm).all() and (rows[:, 0] >= 0).all()
+    # cliques unique
+    assert len(np.unique(mem, axis=0)) == C
+    # weight = f32(f64(conf) * median JI) >= 0.3 * conf; conf is a member's score median
+    assert (r.w > 0).all() and (r.w <= r.conf).all()
+    ctx.close()

@@ -1,0 +1,149 @@
+"""CPU tests of librepic_gc.so's host-side pieces (no GPU needed).
+
+* every symbol declared in include/repic_gc.h is exported
+* the CPython 3.10 hash / set-iteration-order emulation (pyset.h, used on the device for the
+  consensus tie-break, reference get_cliques.py:182-183) agrees with the live interpreter
+* the C++ BOX parser reproduces get_box_coords' acceptance rules (reference common.py:71-114)
+"""
+import ctypes
+import os
+import random
+import re
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+from repic_amd import _lib  # noqa: E402
+from repic_amd.ingest import _py_parse, parse_many  # noqa: E402
+
+
+def test_abi_exports_match_header():
+    hdr = open(os.path.join(ROOT, "include", "repic_gc.h")).read()
+    decl = set(re.findall(r"\b(rgc_[a-z_]+)\s*\(", hdr))
+    assert decl == set(_lib.EXPORTS), decl ^ set(_lib.EXPORTS)
+    so = ctypes.CDLL(_lib.LIB_PATH)
+    for name in decl:
+        assert hasattr(so, name), name
+    assert _lib.abi_version() == 1
+
+
+def _rand_float(rng):
+    r = rng.random()
+    if r < 0.3:
+        return float(rng.randint(-5000, 5000))
+    if r < 0.5:
+        return rng.uniform(-1e4, 1e4)
+    if r < 0.6:
+        return rng.choice([0.0, -0.0, 1.0, -1.0, 0.5, 2.0 ** 60, 1e300, -1e-300, 5e-324,
+                           float("inf"), float("-inf")])
+    if r < 0.8:
+        return round(rng.uniform(0, 4096), rng.randint(0, 6))
+    return rng.uniform(-1, 1) * 10 ** rng.randint(-30, 30)
+
+
+def test_hash_node_matches_cpython():
+    rng = random.Random(1)
+    for _ in range(20000):
+        x, y = _rand_float(rng), _rand_float(rng)
+        i = rng.choice([0, 1, 7, rng.randint(0, 10 ** 6), rng.randint(0, 2 ** 61 + 5)])
+        h = hash((x, y, i)) & 0xFFFFFFFFFFFFFFFF
+        assert _lib.py_hash_node(x, y, i) == h, (x, y, i)
+
+
+def test_set_order_matches_cpython():
+    rng = random.Random(2)
+    for trial in range(30000):
+        n = rng.randint(1, 16)
+        if trial % 3 == 0:   # clustered keys (duplicate coordinates, consecutive ids)
+            base = rng.randint(0, 10 ** 6)
+            keys = [(float(rng.randint(0, 3)), float(rng.randint(0, 3)), base + t)
+                    for t in range(n)]
+        else:
+            keys = [(_rand_float(rng), _rand_float(rng), rng.randint(0, 10 ** 7)) for _ in range(n)]
+        keys = sorted(set(keys))
+        hs = [hash(kk) for kk in keys]
+        got = _lib.py_set_order(hs)
+        want = [keys.index(kk) for kk in set(keys)]
+        assert got == want, (keys, got, want)
+
+
+def _write(tmp_path, name, text, mode="w"):
+    p = os.path.join(str(tmp_path), name)
+    with open(p, mode) as f:
+        f.write(text)
+    return p
+
+
+PARSE_CASES = {
+    "plain": "1 2 3 4 0.5\n10 20 3 4 0.25\n",
+    "crlf": "1 2 3 4 0.5\r\n10 20 3 4 0.25\r\n",
+    "cr_only": "1 2 3 4 0.5\r10 20 3 4 0.25\r",
+    "no_final_newline": "1 2 3 4 0.5\n10 20 3 4 0.25",
+    "header": "x y w h s\n1 2 3 4 0.5\n",
+    "header_only": "x y w h s\n",
+    "blank_first": "\n1 2 3 4 0.5\n",
+    "ws_first": "   \t \n1 2 3 4 0.5\n",
+    "empty": "",
+    "blank_mid": "1 2 3 4 0.5\n\n3 4 5 6 0.1\n",
+    "trailing_blank": "1 2 3 4 0.5\n\n",
+    "six_cols": "1 2 3 4 0.5 extra\n5 6 7 8 0.25 x y\n",
+    "six_and_five": "1 2 3 4 0.5 extra\n5 6 7 8 0.25\n",
+    "four_cols": "1 2 3 4\n",
+    "bad_weight": "1 2 3 4 abc\n",
+    "bad_x": "1 2 3 4 0.5\nzz 6 7 8 0.25\n",
+    "bad_xy_same_row": "1 2 3 4 0.5\nzz qq 7 8 0.25\n",
+    "underscores": "1_000 2_0.5_0 3 4 0.5\n1__0 2 3 4 0.5\n",
+    "specials": "inf -Infinity 3 4 nan\n+1.5e3 .5 3 4 -0.25\n1. -0. 3 4 1e-3\n",
+    "negative_scores": "1 2 3 4 -0.5\n3 4 5 6 2.5\n",
+    "nan_and_neg": "1 2 3 4 nan\n3 4 5 6 -2.5\n",
+    "vt_ff_sep": "1\x0b2\x0c3\x1c4\x1f0.5\n",
+    "tabs": "1\t2\t3\t4\t0.5\n",
+    "exotic_tokens": "0x10 1e 3 4 0.5\n1e5 2E-2 3 4 .5e1\n_1 2 3 4 0.5\n",
+    "nonascii": "1 2 3 4 0.5\n٣ 2 3 4 0.5\n",
+    "bom": "﻿1 2 3 4 0.5\n5 6 7 8 0.25\n",
+}
+
+
+def _python_semantics(path):
+    """What the reference's parse (common.py:71-99) yields for this file."""
+    try:
+        x, y, s, sig = _py_parse(path)
+        return ("ok", x, y, s, sig)
+    except Exception as e:  # noqa: BLE001
+        return (type(e).__name__,)
+
+
+@pytest.mark.parametrize("case", sorted(PARSE_CASES))
+def test_parser_matches_python(case, tmp_path):
+    p = _write(tmp_path, case + ".box", PARSE_CASES[case])
+    want = _python_semantics(p)
+    got = parse_many([p])[0]
+    if want[0] == "ok":
+        assert got.exc is None, got.exc
+        for a, b in zip((got.x, got.y, got.s), want[1:4]):
+            assert np.array_equal(np.asarray(a).view(np.uint64), np.asarray(b).view(np.uint64))
+        assert got.sigmoid == want[4]
+    else:
+        assert got.exc is not None and type(got.exc).__name__ == want[0], (got.exc, want)
+
+
+def test_parser_random_floats_roundtrip(tmp_path):
+    rng = random.Random(3)
+    vals = [_rand_float(rng) for _ in range(3000)]
+    vals = [v for v in vals if np.isfinite(v)]
+    lines = "".join(f"{v!r} {rng.random()!r} 1 1 {rng.random()!r}\n" for v in vals)
+    p = _write(tmp_path, "r.box", lines)
+    got = parse_many([p])[0]
+    assert np.array_equal(np.array(vals).view(np.uint64), got.x.view(np.uint64))
+
+
+def test_sigmoid_vector_equals_scalar_loop():
+    """numpy's vectorised exp gives the same bits as the reference's per-value loop."""
+    rng = np.random.default_rng(4)
+    s = np.concatenate([rng.normal(2, 2, 5000), rng.uniform(-50, 50, 5000)])
+    ref = np.array([1. / (1. + np.exp(-1. * float(v))) for v in s])
+    from repic_amd.ingest import sigmoid
+    assert np.array_equal(sigmoid(s).view(np.uint64), ref.view(np.uint64))
