@@ -54,6 +54,23 @@ def pipeline_bytes(N, E, C, k):
     return 28 * N + 32 * E + C * (20 * k + 12)
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of ``kernel`` from the newest profiles/*_traffic.json written by
+    tools/pmc_traffic.py for THIS library build (sha256 must match), else None."""
+    import glob
+    import hashlib
+    from repic_amd import _lib
+    sha = hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("lib_sha256") == sha and kernel in d.get("kernels", {}):
+            return d["kernels"][kernel]["traffic"], os.path.basename(f)
+    return None, None
+
+
 def cpu_baseline(cfg, mgs, budget_s=12.0):
     """Oracle faithful per-pair loop (oracle/cpu_ref.py, same structure as the reference's
     get_jaccard, get_cliques.py:59-69) on the first micrographs of this workload."""
@@ -167,6 +184,7 @@ def main():
     achieved = dom_bytes / (avg[dom] * 1e-3) / 1e9
     dev_ms = sum(v for k_, v in avg.items() if k_ not in ("d2h", "h2d_meta"))
     pipe = pipeline_bytes(N, E, C, cfg.k)
+    traffic, traffic_src = pmc_traffic(dom)
     out = {
         "metric": "micrographs/sec (get_cliques, whole node) at 1/2/4/8 MI355X; % HBM roofline",
         "value": value, "unit": "micrographs/s", "n_gpus": world, "steps": steps,
@@ -180,7 +198,8 @@ def main():
         "edges_per_sec": tot_e * steps / elapsed,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": None, "alg_bytes_per_launch": dom_bytes,
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "alg_bytes_per_launch": dom_bytes,
                      "avg_launch_ms": avg[dom]},
         "pipeline": {"device_ms_per_step": dev_ms, "alg_bytes": pipe,
                      "achieved_gbs": pipe / (dev_ms * 1e-3) / 1e9,

@@ -21,7 +21,8 @@ from pathlib import Path
 import numpy as np
 
 from .. import _lib
-from ..ingest import DirIndex, list_methods, plan, probe_start_method
+from ..dist import exclusive_offsets, shard_bounds
+from ..ingest import DirIndex, list_methods, micrograph_names, plan, probe_start_method
 from ..pipeline import Batch, run_batch, split_batches
 from ..writers import (consensus_coords, constraint_matrix, multi_out_coords, write_micrograph,
                        write_skip)
@@ -55,25 +56,52 @@ def _del_dir(path):
         shutil.rmtree(p)
 
 
+def _dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
 def main(args):
+    """get_cliques.py:72-229 semantics; under torchrun (WORLD_SIZE > 1) every rank takes a
+    contiguous shard of the micrographs on its own GPU."""
+    world, rank, local = _dist_env()
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        if not dist.is_initialized():
+            dist.init_process_group("gloo")   # control-plane only: 8-byte exchanges
     assert os.path.exists(args.in_dir), "Error - input directory does not exist"
-    _del_dir(args.out_dir)
+    if rank == 0:
+        _del_dir(args.out_dir)
+    if dist is not None:
+        dist.barrier()
     methods = list_methods(args.in_dir)
     Path(args.out_dir).mkdir(parents=True, exist_ok=True)
     listing = getattr(args, "listing", None)     # tests: replay a recorded readdir order
     index = DirIndex(args.in_dir, methods, listing)
     start = probe_start_method(index, methods)
-    print(f"Using {start} BOX files as starting point")
+    if rank == 0:
+        print(f"Using {start} BOX files as starting point")
+    names = micrograph_names(index, methods)
+    lo, hi = 0, len(names)
+    if dist is not None:
+        b = shard_bounds(np.ones(len(names)), world)
+        lo, hi = b[rank], b[rank + 1]
     t_plan = time.time()
-    mgs, crash = plan(args.in_dir, methods, index, n_threads=getattr(args, "threads", None))
+    mgs, crash, consumed = plan(args.in_dir, methods, index, order=names[lo:hi],
+                                n_threads=getattr(args, "threads", None))
+    id_off = 0
+    if dist is not None:
+        id_off, _ = exclusive_offsets(consumed)
+        for mg in mgs:
+            mg.id_base += id_off
     k = len(methods)
     ok = [mg for mg in mgs if mg.status == "ok"]
     t_plan = time.time() - t_plan
     results = {}
     t_dev = 0.0
     if ok:
-        dev = args.device if getattr(args, "device", None) is not None else int(
-            os.environ.get("LOCAL_RANK", "0"))
+        dev = args.device if getattr(args, "device", None) is not None else local
         ctx = _lib.Context(dev)
         counts = [sum(c.n for c in mg.coords) for mg in ok]
         for m0, m1 in split_batches(counts, getattr(args, "batch_boxes", 1 << 25)):
@@ -87,8 +115,24 @@ def main(args):
             for j, mg in enumerate(part):
                 results[id(mg)] = (batch, j, res[j])
         ctx.close()
+    # first micrograph (global index) at which the reference would raise
+    fail = None
+    for i, mg in enumerate(mgs):
+        if mg.status == "crash" or (mg.status == "ok" and
+                                    results[id(mg)][2].status != _lib.OK):
+            fail = lo + i
+            break
+    if dist is not None:
+        from ..dist import first_failure
+        gfail = first_failure(fail)
+    else:
+        gfail = fail
     share = (t_plan + t_dev) / max(1, len(mgs))
-    for mg in mgs:
+    for i, mg in enumerate(mgs):
+        if gfail is not None and lo + i > gfail:
+            break
+        if gfail is not None and lo + i == gfail and fail != gfail:
+            break
         print(f"\n--- {mg.base} ---\n")
         if mg.status == "skip":
             print("Skipping micrograph - not all methods have picked particles...")

@@ -210,14 +210,21 @@ def _glob_path_itself(path: str):
             if not n.startswith(".") and fnmatch.fnmatchcase(n, name)]
 
 
+def micrograph_names(index: DirIndex, methods):
+    """First-picker BOX files in readdir order = the reference's processing order (:108)."""
+    return index.glob(methods[0], "*.box")
+
+
 def plan(in_dir, methods, index: DirIndex, order=None, n_threads=None):
     """Enumerate micrographs in reference order, parse their files and assign box ids.
 
-    Returns ``(micrographs, crash_index)``: processing stops at the first micrograph that
-    would crash the reference (its exception in ``exc``); skipped micrographs still
-    consume the ids of the pickers loaded before the failing one.
+    ``order`` restricts/reorders the first-picker file names (a shard).  Ids start at 0 for
+    the first listed micrograph; a sharded caller adds its global offset.  Returns
+    ``(micrographs, crash_index, consumed)``: processing stops at the first micrograph that
+    would crash the reference (its exception in ``exc``); skipped micrographs still consume
+    the ids of the pickers loaded before the failing one.
     """
-    first = order if order is not None else index.glob(methods[0], "*.box")
+    first = order if order is not None else micrograph_names(index, methods)
     mgs = []
     for name in first:
         base = name.replace(".box", "")
@@ -262,4 +269,4 @@ def plan(in_dir, methods, index: DirIndex, order=None, n_threads=None):
                      for c in coords]
     if crash is not None:
         mgs = mgs[:crash + 1]
-    return mgs, crash
+    return mgs, crash, next_id

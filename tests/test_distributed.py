@@ -1,0 +1,129 @@
+"""Multi-process (world size 2) tests of the sharded path.
+
+CPU (gloo): shard bounds, the global box-id offset exchange, counter reduction and the
+first-failure agreement (repic_amd/dist.py).  GPU: the full CLI under two ranks (both on
+cuda:0) reproduces the single-process goldens, including ids consumed by skipped
+micrographs in an earlier shard and a crash in the middle of the list.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _spawn(code, world, extra_env=None, timeout=240):
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, WORLD_SIZE=str(world), RANK=str(r), LOCAL_RANK="0",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   PYTHONPATH=os.pathsep.join([ROOT, os.path.join(ROOT, "repic-copy_amd"),
+                                               os.path.join(ROOT, "tests")]))
+        env.update(extra_env or {})
+        procs.append(subprocess.Popen([sys.executable, "-c", code], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=timeout)
+        outs.append((p.returncode, o, e))
+    return outs
+
+
+def test_shard_bounds_balanced():
+    from repic_amd.dist import shard_bounds
+    for n in (0, 1, 7, 100):
+        for world in (1, 2, 3, 8):
+            w = np.random.default_rng(n + world).integers(1, 10, size=n)
+            b = shard_bounds(w, world)
+            assert len(b) == world + 1 and b[0] == 0 and b[-1] == n
+            assert all(b[i] <= b[i + 1] for i in range(world))
+
+
+CPU_CODE = r"""
+import json, os, torch.distributed as dist
+from repic_amd.dist import exclusive_offsets, reduce_counts, first_failure
+dist.init_process_group("gloo")
+r = dist.get_rank()
+off, tot = exclusive_offsets(100 + 7 * r)
+cnt = reduce_counts([1, r, 10])
+ff = first_failure(None if r == 0 else 5 + r)
+ff2 = first_failure(None)
+print(json.dumps({"off": off, "tot": tot, "cnt": cnt, "ff": ff, "ff2": ff2}))
+dist.destroy_process_group()
+"""
+
+
+def test_gloo_world2_exchanges():
+    outs = _spawn(CPU_CODE, 2)
+    res = []
+    for rc, o, e in outs:
+        assert rc == 0, e[-2000:]
+        res.append(json.loads(o.strip().splitlines()[-1]))
+    assert res[0]["off"] == 0 and res[1]["off"] == 100
+    assert res[0]["tot"] == res[1]["tot"] == 207
+    assert res[0]["cnt"] == res[1]["cnt"] == [2, 1, 20]
+    assert res[0]["ff"] == res[1]["ff"] == 6
+    assert res[0]["ff2"] is None and res[1]["ff2"] is None
+
+
+GPU_CODE = r"""
+import argparse, builtins, json, os, sys
+from golden_util import load_case, make_inputs
+from repic_amd.commands import get_cliques
+name, root = sys.argv[1], sys.argv[2]
+meta, data = load_case(name)
+in_dir = os.path.join(root, "in")
+out_dir = os.path.join(root, "out")
+a = argparse.Namespace(in_dir=in_dir, out_dir=out_dir, box_size=meta["box"],
+                       multi_out="--multi_out" in meta["flags"], get_cc="--get_cc" in meta["flags"],
+                       batch_boxes=1 << 25, threads=None, device=0, listing=meta["listing"])
+exc = None
+try:
+    get_cliques.main(a)
+except Exception as e:
+    exc = type(e).__name__
+print(json.dumps({"exc": exc}))
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["c1_10017", "skips", "crash_noedges", "ties_getcc"])
+def test_cli_two_ranks_match_golden(name, tmp_path):
+    from golden_util import assert_matches_golden, load_case, make_inputs, read_outputs
+    meta, data = load_case(name)
+    make_inputs(name, str(tmp_path))
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK="0",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   PYTHONPATH=os.pathsep.join([ROOT, os.path.join(ROOT, "repic-copy_amd"),
+                                               os.path.join(ROOT, "tests")]))
+        procs.append(subprocess.Popen([sys.executable, "-c", GPU_CODE, name, str(tmp_path)],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                      text=True))
+    excs = []
+    for p in procs:
+        o, e = p.communicate(timeout=600)
+        assert p.returncode == 0, e[-3000:]
+        excs.append(json.loads(o.strip().splitlines()[-1])["exc"])
+    if meta["exception"]:
+        assert meta["exception"] in excs
+    else:
+        assert excs == [None, None]
+    mgs, arrays = read_outputs(os.path.join(str(tmp_path), "out"), meta)
+    assert_matches_golden(meta, data, mgs, arrays)
