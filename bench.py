@@ -32,9 +32,13 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 DEFAULT_MG = {"C2": 10000, "C3": 1000, "C4": 12500, "C5": 8}
 
 
-def alg_bytes(name, N, E, C, k, V):
+def alg_bytes(name, N, E, C, k, V, n_mg=0):
     """Algorithmic (compulsory) HBM bytes of one launch of each kernel."""
     table = {
+        # fused per-micrograph kernel: read x, y (16 B/box) and the scores of clique vertices
+        # (8 B/vertex); write rows (4k), w, conf, consensus (12) per clique and 56 B of
+        # per-micrograph stats
+        "k_fused": 16 * N + 8 * V + C * (4 * k + 12) + 56 * n_mg,
         "k1_bin": 16 * N + 30 * N,                       # read x,y; write sorted SoA + maps
         "k2_pairs_count": 21 * N + 4 * N,                # read sx,sy,spick,sbox; write count
         "k2_pairs_fill": 21 * N + 8 * N + 12 * E,        # + offsets; write (dst, JI) per edge
@@ -178,11 +182,12 @@ def main():
     steps = args.steps
     value = tot_mg * steps / elapsed
     avg = {k_: v / steps for k_, v in ktimes.items()}
-    kern = {k_: v for k_, v in avg.items() if alg_bytes(k_, N, E, C, cfg.k, V) is not None}
+    kern = {k_: v for k_, v in avg.items()
+            if alg_bytes(k_, N, E, C, cfg.k, V, n_mg) is not None}
     dom = max(kern, key=kern.get)
-    dom_bytes = alg_bytes(dom, N, E, C, cfg.k, V)
+    dom_bytes = alg_bytes(dom, N, E, C, cfg.k, V, n_mg)
     achieved = dom_bytes / (avg[dom] * 1e-3) / 1e9
-    dev_ms = sum(v for k_, v in avg.items() if k_ not in ("d2h", "h2d_meta"))
+    dev_ms = sum(v for k_, v in avg.items() if k_ not in ("d2h", "h2d_meta", "d2h_stats"))
     pipe = pipeline_bytes(N, E, C, cfg.k)
     traffic, traffic_src = pmc_traffic(dom)
     out = {

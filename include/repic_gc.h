@@ -34,6 +34,9 @@ extern "C" {
 #define RGC_F_DEVICE_INPUTS  4u  /* x/y/score are device pointers (HBM-resident) */
 #define RGC_F_HOST_OUTPUTS   8u  /* copy per-clique outputs to pinned host memory */
 #define RGC_F_TIMING        16u  /* record per-kernel HIP events (rgc_kernel_times) */
+#define RGC_F_MEMBERS       32u  /* also return the k member boxes of every clique */
+#define RGC_F_NO_FUSED      64u  /* route every micrograph through the multi-kernel path
+                                    (testing / comparison; outputs are identical) */
 
 /* per-micrograph status (rgc_batch_out.status) */
 #define RGC_OK          0   /* outputs written as in get_cliques.py:215-229 */
@@ -65,13 +68,16 @@ typedef struct rgc_batch_out {
   int32_t* n_nodes;        /* graph nodes (boxes with >= 1 edge) */
   int32_t* n_vert;         /* constraint-matrix rows V (get_cliques.py:164) */
   int64_t* n_edges_mg;     /* JI > 0.3 edges */
-  int64_t* clique_off;     /* [n_mg+1] cliques of mg m are [clique_off[m], clique_off[m+1]) */
+  int64_t* clique_base;    /* cliques of mg m are [clique_base[m], +clique_cnt[m]) in the */
+  int64_t* clique_cnt;     /* per-clique arrays (ranges of different micrographs do not
+                              overlap; their order is unspecified) */
   /* per clique; host (RGC_F_HOST_OUTPUTS) or device pointers */
   int32_t* rows;           /* [C*k] COO row indices of each clique column, ascending */
   float* w;                /* [C] weight vector (get_cliques.py:188-190) */
   float* conf;             /* [C] consensus confidences (:186-187) */
   int32_t* consensus;      /* [C] global box index of the consensus box (:182-183) */
-  int32_t* members;        /* [C*k] global box index of each member, picker order */
+  int32_t* members;        /* [C*k] global box index of each member, picker order
+                              (with RGC_F_MEMBERS or RGC_F_MULTI_OUT, else NULL) */
   uint8_t* order;          /* [C*k] networkx node-iteration order as picker indices
                               (only with RGC_F_MULTI_OUT, else NULL) */
 } rgc_batch_out;

@@ -1,11 +1,20 @@
 // rgc_abi.cpp — host orchestration of the batched get_cliques pipeline + the C-ABI
-// (include/repic_gc.h).  One context per device/stream; device workspace is a grow-only
-// arena so steady-state calls do no hipMalloc.  Data-dependent sizes (edges, cliques) are
-// resolved by two-phase count -> scan -> fill with one small D2H read per phase.
+// (include/repic_gc.h).
+//
+// rgc_run:
+//   1. size-class every micrograph by its box count; each class is one launch of the fused
+//      per-micrograph kernel (rgc_fused.hip) with an LDS image sized for the class;
+//   2. one sync: read per-micrograph stats and the clique reservation cursor; if the output
+//      arrays were too small, grow them and re-run the fused launches (first calls only);
+//   3. micrographs too large for LDS (or whose edges overflowed the class's LDS edge
+//      capacity) are gathered into a compact sub-batch and run through the multi-kernel
+//      pipeline (rgc_kernels.hip), writing after the fused outputs.
+// One context per device/stream; device workspace is a grow-only arena.
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -28,23 +37,40 @@ static int fail(const std::string& msg) {
     if (e_ != hipSuccess)                                                              \
       return fail(std::string(#expr) + ": " + hipGetErrorString(e_));                   \
   } while (0)
+#define TRY(expr)           \
+  do {                      \
+    int r_ = (expr);        \
+    if (r_ != 0) return r_; \
+  } while (0)
 
 namespace {
 
 enum DevBufId {
-  D_BOXOFF, D_CELLOFF, D_IDBASE, D_X, D_Y, D_S, D_GRID, D_CELLSTART, D_SX, D_SY, D_SBOX,
-  D_SPICK, D_SMG, D_BMG, D_BPICK, D_FWDCNT, D_FWDOFF, D_TILES, D_TOTAL, D_EDST, D_EJI,
-  D_PARENT, D_HASEDGE, D_CSIZE, D_STAT, D_INSKEY, D_COMPMIN, D_CCOUNT, D_COFF, D_MEMBERS,
-  D_W, D_CONF, D_CONS, D_ORDER, D_INCL, D_VLIST, D_VSORT, D_VROW, D_ROWS, D_MGOFF, D_COUNT
+  // fused path / whole batch
+  D_FBOXOFF, D_FIDBASE, D_MGLIST, D_FSTAT, D_CURSOR, D_X, D_Y, D_S,
+  // outputs
+  D_ROWS, D_W, D_CONF, D_CONS, D_MEMBERS, D_ORDER,
+  // multi-kernel path (sub-batch)
+  D_SUBMG, D_SUBX, D_SUBY, D_SUBS, D_ORIG,
+  D_BOXOFF, D_CELLOFF, D_IDBASE, D_GRID, D_CELLSTART, D_SX, D_SY, D_SBOX, D_SPICK, D_SMG, D_BMG,
+  D_BPICK, D_FWDCNT, D_FWDOFF, D_TILES, D_TOTAL, D_EDST, D_EJI, D_PARENT, D_HASEDGE, D_CSIZE,
+  D_STAT, D_INSKEY, D_COMPMIN, D_CCOUNT, D_COFF, D_INCL, D_VLIST, D_VSORT, D_VROW, D_MGOFF,
+  D_COUNT
 };
 enum HostBufId {
-  H_STAGE, H_TOTAL, H_STAT, H_MGOFF, H_ROWS, H_W, H_CONF, H_CONS, H_MEMBERS, H_ORDER, H_COUNT
+  H_FSTAGE, H_STAGE, H_TOTAL, H_FSTAT, H_STAT, H_MGOFF, H_ROWS, H_W, H_CONF, H_CONS, H_MEMBERS,
+  H_ORDER, H_COUNT
 };
 
 struct Buf {
   void* p = nullptr;
   size_t cap = 0;
 };
+
+// Fused size classes: boxes per micrograph and forward-edge capacity per class.
+constexpr int N_CLASSES = 5;
+constexpr int CLASS_N[N_CLASSES] = {256, 512, 1024, 2048, 3200};
+inline int class_ecap(int nmax) { return 4 * nmax; }
 
 }  // namespace
 
@@ -60,21 +86,26 @@ struct rgc_ctx {
   bool timing = false;
   std::vector<float> times;
   std::vector<const char*> time_names;
+  int64_t cap_cliques = 0;   // capacity of the per-clique output arrays
   // per-micrograph host outputs
   std::vector<int32_t> status, cc_max, cc_cnt, n_nodes, n_vert;
-  std::vector<int64_t> n_edges_mg, clique_off;
+  std::vector<int64_t> n_edges_mg, clique_base, clique_cnt;
 };
 
-static int ensure_dev(rgc_ctx* c, int id, size_t bytes) {
+static int ensure_dev(rgc_ctx* c, int id, size_t bytes, size_t keep = 0) {
   Buf& b = c->d[id];
   if (bytes == 0) bytes = 16;
   if (b.cap >= bytes) return 0;
-  if (b.p) HIPCHK(hipFree(b.p));
   size_t cap = std::max(bytes, b.cap + b.cap / 2);
   cap = (cap + 255) & ~(size_t)255;
-  b.p = nullptr;
-  b.cap = 0;
-  HIPCHK(hipMalloc(&b.p, cap));
+  void* p = nullptr;
+  HIPCHK(hipMalloc(&p, cap));
+  if (b.p && keep) {
+    HIPCHK(hipMemcpyAsync(p, b.p, std::min(keep, b.cap), hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
+  if (b.p) HIPCHK(hipFree(b.p));
+  b.p = p;
   b.cap = cap;
   return 0;
 }
@@ -111,56 +142,32 @@ static int mark(rgc_ctx* c, const char* name) {
   return 0;
 }
 
-#define TRY(expr)        \
-  do {                   \
-    int r_ = (expr);     \
-    if (r_ != 0) return r_; \
-  } while (0)
+// Grow the per-clique output arrays to `need` cliques, keeping the first `keep` cliques.
+static int ensure_outputs(rgc_ctx* c, int64_t need, int64_t keep, int k, bool members,
+                          bool multi) {
+  TRY(ensure_dev(c, D_ROWS, need * k * 4, keep * k * 4));
+  TRY(ensure_dev(c, D_W, need * 4, keep * 4));
+  TRY(ensure_dev(c, D_CONF, need * 4, keep * 4));
+  TRY(ensure_dev(c, D_CONS, need * 4, keep * 4));
+  if (members) TRY(ensure_dev(c, D_MEMBERS, need * k * 4, keep * k * 4));
+  if (multi) TRY(ensure_dev(c, D_ORDER, need * k, keep * k));
+  return 0;
+}
 
-static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
-  const int n_mg = in->n_mg, k = in->k;
-  const uint32_t flags = in->flags;
-  if (n_mg < 0) return fail("n_mg < 0");
-  if (k < 1 || k > MAX_K) return fail("k (number of pickers) must be in 1..8");
-  if (in->box_size > (1LL << 26)) return fail("box_size too large (> 2^26)");
-  const int64_t N = n_mg ? in->box_off[(int64_t)n_mg * k] : 0;
-  if (N >= (1LL << 31) - 1) return fail("too many boxes in one batch (>= 2^31)");
-  const int get_cc = (flags & RGC_F_GET_CC) ? 1 : 0;
-  const int multi = (flags & RGC_F_MULTI_OUT) ? 1 : 0;
-  const double B = (double)in->box_size;
-  const double two_b2 = (double)(2 * in->box_size * in->box_size);
-  c->timing = (flags & RGC_F_TIMING) != 0;
-  c->n_ev = 0;
-
-  c->status.assign(n_mg, 0);
-  c->cc_max.assign(n_mg, 0);
-  c->cc_cnt.assign(n_mg, 0);
-  c->n_nodes.assign(n_mg, 0);
-  c->n_vert.assign(n_mg, 0);
-  c->n_edges_mg.assign(n_mg, 0);
-  c->clique_off.assign(n_mg + 1, 0);
-  std::memset(out, 0, sizeof(*out));
-  out->status = c->status.data();
-  out->cc_max = c->cc_max.data();
-  out->cc_cnt = c->cc_cnt.data();
-  out->n_nodes = c->n_nodes.data();
-  out->n_vert = c->n_vert.data();
-  out->n_edges_mg = c->n_edges_mg.data();
-  out->clique_off = c->clique_off.data();
-  out->n_boxes = N;
-  if (n_mg == 0) return 0;
-  if (k == 1) {  // no picker pairs -> no edges -> reference ValueError on every micrograph
-    std::fill(c->status.begin(), c->status.end(), RGC_NO_EDGES);
-    return 0;
-  }
-
-  // ---- small per-micrograph arrays (host -> device through one pinned staging buffer)
+// ---------------------------------------------------------------------------- multi-kernel path
+// Runs the multi-kernel pipeline on a (sub-)batch whose x/y/score are device arrays, writing
+// per-clique outputs at [out_base, out_base + C).  Fills st_out[n_mg] (clique_base/cnt set).
+static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int get_cc, int multi,
+                     const int64_t* box_off, const int64_t* id_base, const double* x,
+                     const double* y, const double* sc, int64_t out_base,
+                     std::vector<MgStat>& st_out, int64_t* C_out, int64_t* E_out) {
+  const int64_t N = box_off[(int64_t)n_mg * k];
   const size_t nbo = (size_t)n_mg * k + 1;
   std::vector<int32_t> cell_off(n_mg + 1);
   int64_t cells = 0;
   for (int m = 0; m < n_mg; ++m) {
     cell_off[m] = (int32_t)cells;
-    const int64_t nm = in->box_off[(int64_t)(m + 1) * k] - in->box_off[(int64_t)m * k];
+    const int64_t nm = box_off[(int64_t)(m + 1) * k] - box_off[(int64_t)m * k];
     cells += std::min<int64_t>(nm + 1, CELL_CAP - 1) + 2;
   }
   cell_off[n_mg] = (int32_t)cells;
@@ -171,9 +178,9 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   int32_t* st_co = st_bo + nbo;
   int64_t* st_id = reinterpret_cast<int64_t*>(
       (reinterpret_cast<uintptr_t>(st_co + n_mg + 1) + 7) & ~(uintptr_t)7);
-  for (size_t i = 0; i < nbo; ++i) st_bo[i] = (int32_t)in->box_off[i];
+  for (size_t i = 0; i < nbo; ++i) st_bo[i] = (int32_t)box_off[i];
   std::memcpy(st_co, cell_off.data(), (n_mg + 1) * 4);
-  std::memcpy(st_id, in->id_base, n_mg * 8);
+  std::memcpy(st_id, id_base, n_mg * 8);
 
   TRY(ensure_dev(c, D_BOXOFF, nbo * 4));
   TRY(ensure_dev(c, D_CELLOFF, (n_mg + 1) * 4));
@@ -189,8 +196,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   TRY(ensure_dev(c, D_BPICK, N));
   TRY(ensure_dev(c, D_FWDCNT, N * 4));
   TRY(ensure_dev(c, D_FWDOFF, (N + 1) * 8));
-  const int64_t ntile = scan_tiles_needed(N + 1);
-  TRY(ensure_dev(c, D_TILES, ntile * 8));
+  TRY(ensure_dev(c, D_TILES, scan_tiles_needed(N + 1) * 8));
   TRY(ensure_dev(c, D_TOTAL, 16));
   TRY(ensure_dev(c, D_PARENT, N * 4));
   TRY(ensure_dev(c, D_HASEDGE, N));
@@ -214,18 +220,6 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   HIPCHK(hipMemcpyAsync(D<void>(c, D_BOXOFF), st_bo, nbo * 4, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(D<void>(c, D_CELLOFF), st_co, (n_mg + 1) * 4, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(D<void>(c, D_IDBASE), st_id, n_mg * 8, hipMemcpyHostToDevice, s));
-  const double *x = in->x, *y = in->y, *sc = in->score;
-  if (!(flags & RGC_F_DEVICE_INPUTS)) {
-    TRY(ensure_dev(c, D_X, N * 8));
-    TRY(ensure_dev(c, D_Y, N * 8));
-    TRY(ensure_dev(c, D_S, N * 8));
-    HIPCHK(hipMemcpyAsync(D<void>(c, D_X), in->x, N * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(D<void>(c, D_Y), in->y, N * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(D<void>(c, D_S), in->score, N * 8, hipMemcpyHostToDevice, s));
-    x = D<double>(c, D_X);
-    y = D<double>(c, D_Y);
-    sc = D<double>(c, D_S);
-  }
   TRY(mark(c, "memset"));
   HIPCHK(hipMemsetAsync(D<void>(c, D_HASEDGE), 0, N, s));
   HIPCHK(hipMemsetAsync(D<void>(c, D_CSIZE), 0, N * 4, s));
@@ -252,7 +246,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
   const int64_t E = H<int64_t>(c, H_TOTAL)[0];
-  out->n_edges = E;
+  *E_out = E;
   TRY(ensure_dev(c, D_EDST, E * 4));
   TRY(ensure_dev(c, D_EJI, E * 8));
   TRY(mark(c, "k2_pairs_fill"));
@@ -291,75 +285,282 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
   const int64_t C = H<int64_t>(c, H_TOTAL)[0];
-  out->n_cliques = C;
-  TRY(ensure_dev(c, D_MEMBERS, C * k * 4));
-  TRY(ensure_dev(c, D_W, C * 4));
-  TRY(ensure_dev(c, D_CONF, C * 4));
-  TRY(ensure_dev(c, D_CONS, C * 4));
-  TRY(ensure_dev(c, D_ROWS, C * k * 4));
-  if (multi) TRY(ensure_dev(c, D_ORDER, C * k));
-  A.members = D<int32_t>(c, D_MEMBERS); A.w = D<float>(c, D_W); A.conf = D<float>(c, D_CONF);
-  A.consensus = D<int32_t>(c, D_CONS); A.order = multi ? D<uint8_t>(c, D_ORDER) : nullptr;
+  *C_out = C;
+  TRY(ensure_outputs(c, out_base + C, out_base, k, true, multi != 0));
+  A.members = D<int32_t>(c, D_MEMBERS) + out_base * k;
+  A.w = D<float>(c, D_W) + out_base;
+  A.conf = D<float>(c, D_CONF) + out_base;
+  A.consensus = D<int32_t>(c, D_CONS) + out_base;
+  A.order = multi ? D<uint8_t>(c, D_ORDER) + out_base * k : nullptr;
   TRY(mark(c, "k5_cliques_fill"));
   launch_cliques(s, true, (int)N, A);
   TRY(mark(c, "k7_rank"));
   launch_rank(s, n_mg, k, bo, x, y, D<uint8_t>(c, D_INCL), D<int32_t>(c, D_VLIST),
               D<int32_t>(c, D_VSORT), D<int32_t>(c, D_VROW), D<MgStat>(c, D_STAT));
   TRY(mark(c, "k7_rows"));
-  launch_rows(s, k, C, D<int32_t>(c, D_MEMBERS), D<int32_t>(c, D_VROW), D<int32_t>(c, D_ROWS));
+  launch_rows(s, k, C, A.members, D<int32_t>(c, D_VROW), D<int32_t>(c, D_ROWS) + out_base * k);
   TRY(mark(c, "k_mg_offsets"));
   launch_mg_offsets(s, n_mg, k, bo, D<int64_t>(c, D_COFF), D<int64_t>(c, D_MGOFF));
-  TRY(mark(c, "d2h"));
   HIPCHK(hipMemcpyAsync(H<void>(c, H_STAT), D<void>(c, D_STAT), n_mg * sizeof(MgStat),
                         hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOFF), D<void>(c, D_MGOFF), (n_mg + 1) * 8,
                         hipMemcpyDeviceToHost, s));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));
+  const MgStat* st = H<MgStat>(c, H_STAT);
+  const int64_t* mo = H<int64_t>(c, H_MGOFF);
+  st_out.assign(st, st + n_mg);
+  for (int m = 0; m < n_mg; ++m) {
+    st_out[m].clique_base = out_base + mo[m];
+    st_out[m].clique_cnt = mo[m + 1] - mo[m];
+    if (st_out[m].status == RGC_OK && st_out[m].clique_cnt == 0) st_out[m].status = RGC_NO_CLIQUES;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------- rgc_run
+static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
+  const int n_mg = in->n_mg, k = in->k;
+  const uint32_t flags = in->flags;
+  if (n_mg < 0) return fail("n_mg < 0");
+  if (k < 1 || k > MAX_K) return fail("k (number of pickers) must be in 1..8");
+  if (in->box_size > (1LL << 26)) return fail("box_size too large (> 2^26)");
+  const int64_t N = n_mg ? in->box_off[(int64_t)n_mg * k] : 0;
+  if (N >= (1LL << 31) - 1) return fail("too many boxes in one batch (>= 2^31)");
+  const int get_cc = (flags & RGC_F_GET_CC) ? 1 : 0;
+  const int multi = (flags & RGC_F_MULTI_OUT) ? 1 : 0;
+  const bool want_members = (flags & (RGC_F_MEMBERS | RGC_F_MULTI_OUT)) != 0;
+  const double B = (double)in->box_size;
+  const double two_b2 = (double)(2 * in->box_size * in->box_size);
+  c->timing = (flags & RGC_F_TIMING) != 0;
+  c->n_ev = 0;
+
+  c->status.assign(n_mg, 0);
+  c->cc_max.assign(n_mg, 0);
+  c->cc_cnt.assign(n_mg, 0);
+  c->n_nodes.assign(n_mg, 0);
+  c->n_vert.assign(n_mg, 0);
+  c->n_edges_mg.assign(n_mg, 0);
+  c->clique_base.assign(n_mg, 0);
+  c->clique_cnt.assign(n_mg, 0);
+  std::memset(out, 0, sizeof(*out));
+  out->status = c->status.data();
+  out->cc_max = c->cc_max.data();
+  out->cc_cnt = c->cc_cnt.data();
+  out->n_nodes = c->n_nodes.data();
+  out->n_vert = c->n_vert.data();
+  out->n_edges_mg = c->n_edges_mg.data();
+  out->clique_base = c->clique_base.data();
+  out->clique_cnt = c->clique_cnt.data();
+  out->n_boxes = N;
+  if (n_mg == 0) return 0;
+  if (k == 1) {  // no picker pairs -> no edges -> reference ValueError on every micrograph
+    std::fill(c->status.begin(), c->status.end(), RGC_NO_EDGES);
+    return 0;
+  }
+  hipStream_t s = c->stream;
+
+  // ---- classify micrographs
+  std::vector<int32_t> cls_list[N_CLASSES];
+  std::vector<int32_t> big;
+  const bool no_fused = (flags & RGC_F_NO_FUSED) != 0;
+  for (int m = 0; m < n_mg; ++m) {
+    const int64_t nm = in->box_off[(int64_t)(m + 1) * k] - in->box_off[(int64_t)m * k];
+    int cl = -1;
+    if (!no_fused)
+      for (int q = 0; q < N_CLASSES; ++q)
+        if (nm <= CLASS_N[q]) { cl = q; break; }
+    if (cl < 0) big.push_back(m);
+    else cls_list[cl].push_back(m);
+  }
+  const int n_fused = n_mg - (int)big.size();
+
+  // ---- inputs on device
+  const double *x = in->x, *y = in->y, *sc = in->score;
+  const size_t nbo = (size_t)n_mg * k + 1;
+  const size_t fstage = nbo * 4 + n_mg * 8 + n_mg * 4 + 64;
+  TRY(ensure_host(c, H_FSTAGE, fstage));
+  int32_t* f_bo = H<int32_t>(c, H_FSTAGE);
+  int64_t* f_id = reinterpret_cast<int64_t*>(
+      (reinterpret_cast<uintptr_t>(f_bo + nbo) + 7) & ~(uintptr_t)7);
+  int32_t* f_ml = reinterpret_cast<int32_t*>(f_id + n_mg);
+  for (size_t i = 0; i < nbo; ++i) f_bo[i] = (int32_t)in->box_off[i];
+  std::memcpy(f_id, in->id_base, n_mg * 8);
+  {
+    int o = 0;
+    for (int q = 0; q < N_CLASSES; ++q)
+      for (int32_t m : cls_list[q]) f_ml[o++] = m;
+  }
+  TRY(ensure_dev(c, D_FBOXOFF, nbo * 4));
+  TRY(ensure_dev(c, D_FIDBASE, n_mg * 8));
+  TRY(ensure_dev(c, D_MGLIST, n_mg * 4 + 4));
+  TRY(ensure_dev(c, D_FSTAT, n_mg * sizeof(MgStat)));
+  TRY(ensure_dev(c, D_CURSOR, 16));
+  TRY(ensure_host(c, H_FSTAT, n_mg * sizeof(MgStat)));
+  TRY(ensure_host(c, H_TOTAL, 16));
+  TRY(mark(c, "h2d_meta"));
+  HIPCHK(hipMemcpyAsync(D<void>(c, D_FBOXOFF), f_bo, nbo * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(D<void>(c, D_FIDBASE), f_id, n_mg * 8, hipMemcpyHostToDevice, s));
+  if (n_fused) HIPCHK(hipMemcpyAsync(D<void>(c, D_MGLIST), f_ml, n_fused * 4, hipMemcpyHostToDevice, s));
+  if (!(flags & RGC_F_DEVICE_INPUTS)) {
+    TRY(ensure_dev(c, D_X, N * 8));
+    TRY(ensure_dev(c, D_Y, N * 8));
+    TRY(ensure_dev(c, D_S, N * 8));
+    HIPCHK(hipMemcpyAsync(D<void>(c, D_X), in->x, N * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(D<void>(c, D_Y), in->y, N * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(D<void>(c, D_S), in->score, N * 8, hipMemcpyHostToDevice, s));
+    x = D<double>(c, D_X);
+    y = D<double>(c, D_Y);
+    sc = D<double>(c, D_S);
+  }
+
+  std::vector<MgStat> st(n_mg);
+  int64_t fused_total = 0;
+  int64_t E_total = 0;
+  std::vector<int32_t> deferred = big;
+  if (n_fused) {
+    if (c->cap_cliques < 4096) c->cap_cliques = std::max<int64_t>(4096, N);
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      TRY(ensure_outputs(c, c->cap_cliques, 0, k, want_members, multi != 0));
+      HIPCHK(hipMemsetAsync(D<void>(c, D_CURSOR), 0, 16, s));
+      FusedArgs A;
+      A.k = k; A.flags = get_cc | (multi << 1) | (want_members ? 32 : 0);
+      A.B = B; A.two_b2 = two_b2;
+      A.box_off = D<int32_t>(c, D_FBOXOFF); A.id_base = D<int64_t>(c, D_FIDBASE);
+      A.x = x; A.y = y; A.score = sc; A.st = D<MgStat>(c, D_FSTAT);
+      A.cursor = D<unsigned long long>(c, D_CURSOR); A.cap = c->cap_cliques;
+      A.rows = D<int32_t>(c, D_ROWS); A.w = D<float>(c, D_W); A.conf = D<float>(c, D_CONF);
+      A.consensus = D<int32_t>(c, D_CONS);
+      A.members = want_members ? D<int32_t>(c, D_MEMBERS) : nullptr;
+      A.order = multi ? D<uint8_t>(c, D_ORDER) : nullptr;
+      int o = 0;
+      for (int q = 0; q < N_CLASSES; ++q) {
+        const int nb = (int)cls_list[q].size();
+        if (!nb) continue;
+        A.nmax = CLASS_N[q];
+        A.ecap = class_ecap(CLASS_N[q]);
+        A.mg_list = D<int32_t>(c, D_MGLIST) + o;
+        TRY(mark(c, "k_fused"));
+        if (launch_fused(s, nb, fused_lds_bytes(A.nmax, A.ecap), A) != 0)
+          return fail("fused kernel launch failed");
+        o += nb;
+      }
+      TRY(mark(c, "d2h_stats"));
+      HIPCHK(hipMemcpyAsync(H<void>(c, H_FSTAT), D<void>(c, D_FSTAT), n_mg * sizeof(MgStat),
+                            hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(H<void>(c, H_TOTAL), D<void>(c, D_CURSOR), 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipStreamSynchronize(s));
+      fused_total = (int64_t)H<unsigned long long>(c, H_TOTAL)[0];
+      if (fused_total <= c->cap_cliques) break;
+      c->cap_cliques = fused_total + fused_total / 8 + 1024;   // grow and re-run once
+      c->n_ev = 0;
+    }
+    const MgStat* fs = H<MgStat>(c, H_FSTAT);
+    for (int q = 0; q < N_CLASSES; ++q)
+      for (int32_t m : cls_list[q]) {
+        st[m] = fs[m];
+        if (fs[m].status == RGC_ST_OVERFLOW) return fail("internal: output overflow after regrow");
+        if (fs[m].status == RGC_ST_DEFER) deferred.push_back(m);
+        else E_total += fs[m].n_edges;
+      }
+  }
+
+  int64_t C_total = fused_total;
+  if (!deferred.empty()) {
+    std::sort(deferred.begin(), deferred.end());
+    const int ns = (int)deferred.size();
+    std::vector<int64_t> sbo((size_t)ns * k + 1), sid(ns);
+    std::vector<int32_t> sbo32((size_t)ns * k + 1);
+    int64_t acc = 0;
+    for (int i = 0; i < ns; ++i) {
+      const int m = deferred[i];
+      for (int p = 0; p < k; ++p) {
+        sbo[(size_t)i * k + p] = acc;
+        acc += in->box_off[(int64_t)m * k + p + 1] - in->box_off[(int64_t)m * k + p];
+      }
+      sid[i] = in->id_base[m];
+    }
+    sbo[(size_t)ns * k] = acc;
+    for (size_t i = 0; i < sbo.size(); ++i) sbo32[i] = (int32_t)sbo[i];
+    TRY(ensure_dev(c, D_SUBMG, ns * 4));
+    TRY(ensure_dev(c, D_SUBX, acc * 8));
+    TRY(ensure_dev(c, D_SUBY, acc * 8));
+    TRY(ensure_dev(c, D_SUBS, acc * 8));
+    TRY(ensure_dev(c, D_ORIG, acc * 4));
+    TRY(ensure_dev(c, D_BOXOFF, sbo32.size() * 4));
+    HIPCHK(hipMemcpy(D<void>(c, D_SUBMG), deferred.data(), ns * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(D<void>(c, D_BOXOFF), sbo32.data(), sbo32.size() * 4, hipMemcpyHostToDevice));
+    TRY(mark(c, "k_gather"));
+    launch_gather(s, ns, k, D<int32_t>(c, D_SUBMG), D<int32_t>(c, D_FBOXOFF), D<int32_t>(c, D_BOXOFF),
+                  x, y, sc, D<double>(c, D_SUBX), D<double>(c, D_SUBY), D<double>(c, D_SUBS),
+                  D<int32_t>(c, D_ORIG));
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<MgStat> sst;
+    int64_t Cm = 0, Em = 0;
+    TRY(run_multi(c, ns, k, B, two_b2, get_cc, multi, sbo.data(), sid.data(),
+                  D<double>(c, D_SUBX), D<double>(c, D_SUBY), D<double>(c, D_SUBS), fused_total, sst,
+                  &Cm, &Em));
+    TRY(mark(c, "k_remap"));
+    launch_remap(s, Cm, k, D<int32_t>(c, D_ORIG), D<int32_t>(c, D_CONS) + fused_total,
+                 D<int32_t>(c, D_MEMBERS) + fused_total * k);
+    for (int i = 0; i < ns; ++i) st[deferred[i]] = sst[i];
+    C_total += Cm;
+    E_total += Em;
+  }
+  out->n_cliques = C_total;
+  out->n_edges = E_total;
+
   if (flags & RGC_F_HOST_OUTPUTS) {
+    TRY(mark(c, "d2h"));
+    const int64_t C = C_total;
     TRY(ensure_host(c, H_ROWS, C * k * 4));
     TRY(ensure_host(c, H_W, C * 4));
     TRY(ensure_host(c, H_CONF, C * 4));
     TRY(ensure_host(c, H_CONS, C * 4));
-    TRY(ensure_host(c, H_MEMBERS, C * k * 4));
+    if (want_members) TRY(ensure_host(c, H_MEMBERS, C * k * 4));
     if (multi) TRY(ensure_host(c, H_ORDER, C * k));
-    HIPCHK(hipMemcpyAsync(H<void>(c, H_ROWS), D<void>(c, D_ROWS), C * k * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(H<void>(c, H_W), D<void>(c, D_W), C * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(H<void>(c, H_CONF), D<void>(c, D_CONF), C * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(H<void>(c, H_CONS), D<void>(c, D_CONS), C * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(H<void>(c, H_MEMBERS), D<void>(c, D_MEMBERS), C * k * 4,
-                          hipMemcpyDeviceToHost, s));
-    if (multi)
-      HIPCHK(hipMemcpyAsync(H<void>(c, H_ORDER), D<void>(c, D_ORDER), C * k, hipMemcpyDeviceToHost, s));
+    if (C) {
+      HIPCHK(hipMemcpyAsync(H<void>(c, H_ROWS), D<void>(c, D_ROWS), C * k * 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(H<void>(c, H_W), D<void>(c, D_W), C * 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(H<void>(c, H_CONF), D<void>(c, D_CONF), C * 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(H<void>(c, H_CONS), D<void>(c, D_CONS), C * 4, hipMemcpyDeviceToHost, s));
+      if (want_members)
+        HIPCHK(hipMemcpyAsync(H<void>(c, H_MEMBERS), D<void>(c, D_MEMBERS), C * k * 4,
+                              hipMemcpyDeviceToHost, s));
+      if (multi)
+        HIPCHK(hipMemcpyAsync(H<void>(c, H_ORDER), D<void>(c, D_ORDER), C * k, hipMemcpyDeviceToHost, s));
+    }
     out->rows = H<int32_t>(c, H_ROWS);
     out->w = H<float>(c, H_W);
     out->conf = H<float>(c, H_CONF);
     out->consensus = H<int32_t>(c, H_CONS);
-    out->members = H<int32_t>(c, H_MEMBERS);
+    out->members = want_members ? H<int32_t>(c, H_MEMBERS) : nullptr;
     out->order = multi ? H<uint8_t>(c, H_ORDER) : nullptr;
   } else {
     out->rows = D<int32_t>(c, D_ROWS);
     out->w = D<float>(c, D_W);
     out->conf = D<float>(c, D_CONF);
     out->consensus = D<int32_t>(c, D_CONS);
-    out->members = D<int32_t>(c, D_MEMBERS);
+    out->members = want_members ? D<int32_t>(c, D_MEMBERS) : nullptr;
     out->order = multi ? D<uint8_t>(c, D_ORDER) : nullptr;
   }
   TRY(mark(c, "end"));
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
 
-  const MgStat* st = H<MgStat>(c, H_STAT);
-  const int64_t* mo = H<int64_t>(c, H_MGOFF);
   for (int m = 0; m < n_mg; ++m) {
-    c->status[m] = st[m].status;
+    int stt = st[m].status;
+    if (stt == RGC_OK && st[m].clique_cnt == 0) stt = RGC_NO_CLIQUES;
+    c->status[m] = stt;
     c->cc_max[m] = st[m].cc_max;
     c->cc_cnt[m] = st[m].cc_cnt;
     c->n_nodes[m] = st[m].n_nodes;
     c->n_vert[m] = st[m].n_vert;
     c->n_edges_mg[m] = st[m].n_edges;
-    c->clique_off[m] = mo[m];
-    if (c->status[m] == RGC_OK && mo[m + 1] == mo[m]) c->status[m] = RGC_NO_CLIQUES;
+    c->clique_base[m] = st[m].clique_base;
+    c->clique_cnt[m] = stt == RGC_OK ? st[m].clique_cnt : 0;
   }
-  c->clique_off[n_mg] = mo[n_mg];
 
   if (c->timing) {
     c->times.clear();

@@ -19,8 +19,51 @@ struct MgGrid {
 // Per-micrograph results.
 struct MgStat {
   int64_t n_edges;
+  int64_t clique_base, clique_cnt;   // output range (fused path; host fills it for multi)
   int n_nodes, cc_cnt, cc_max, status, target, n_vert;
 };
+
+// internal per-micrograph status codes (0..2 are the public RGC_* codes)
+constexpr int RGC_ST_NO_EDGES = 1;
+constexpr int RGC_ST_NO_CLIQUES = 2;
+constexpr int RGC_ST_DEFER = 3;      // does not fit the fused kernel's LDS capacities
+constexpr int RGC_ST_OVERFLOW = 4;   // output capacity exceeded: host grows and re-runs
+
+// LDS layout of the fused kernel for a size class (byte offsets into dynamic LDS)
+struct FusedLayout {
+  int off_xs, off_ys, off_cstart, off_cnt, off_fwd, off_parent, off_citems, off_vrank, off_flags,
+      off_dst, total;
+};
+
+struct FusedArgs {
+  int k, flags;                 // flags: bit0 get_cc, bit1 multi_out, bit5 members
+  double B, two_b2;
+  int nmax, ecap;               // LDS capacities of this launch (boxes, forward edges)
+  const int32_t* mg_list;       // micrographs of this size class
+  const int32_t* box_off;
+  const int64_t* id_base;
+  const double* x;
+  const double* y;
+  const double* score;
+  MgStat* st;
+  unsigned long long* cursor;   // clique-range reservation counter
+  int64_t cap;                  // clique capacity of the output arrays
+  int32_t* rows;
+  float* w;
+  float* conf;
+  int32_t* consensus;
+  int32_t* members;
+  uint8_t* order;
+};
+
+int fused_lds_bytes(int nmax, int ecap);
+int launch_fused(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArgs& A);
+void launch_gather(hipStream_t stream, int n_sub, int k, const int32_t* sub_mg,
+                   const int32_t* box_off, const int32_t* sub_box_off, const double* x,
+                   const double* y, const double* s, double* ox, double* oy, double* os,
+                   int32_t* orig);
+void launch_remap(hipStream_t stream, int64_t C, int k, const int32_t* orig, int32_t* consensus,
+                  int32_t* members);
 
 struct CliqueArgsHost {
   int k;

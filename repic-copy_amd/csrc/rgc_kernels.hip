@@ -22,92 +22,10 @@
 #include <stdint.h>
 #include <math.h>
 
-#include "pyset.h"
+#include "rgc_device.h"
 #include "rgc_kernels.h"
 
 namespace rgc {
-
-constexpr int WG = 256;
-constexpr int NW = WG / 64;
-
-// ----------------------------------------------------------------------------- helpers
-template <typename T>
-__device__ __forceinline__ T wave_min(T v) {
-  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-  return v;
-}
-template <typename T>
-__device__ __forceinline__ T wave_max(T v) {
-  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-  return v;
-}
-
-__device__ __forceinline__ double block_min(double v, double* lds) {
-  v = wave_min(v);
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
-  __syncthreads();
-  double r = lds[0];
-  for (int i = 1; i < NW; ++i) r = fmin(r, lds[i]);
-  return r;
-}
-__device__ __forceinline__ double block_max(double v, double* lds) {
-  v = wave_max(v);
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
-  __syncthreads();
-  double r = lds[0];
-  for (int i = 1; i < NW; ++i) r = fmax(r, lds[i]);
-  return r;
-}
-
-__device__ __forceinline__ int64_t block_sum64(int64_t v, int64_t* lds) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
-  __syncthreads();
-  int64_t r = 0;
-  for (int i = 0; i < NW; ++i) r += lds[i];
-  return r;
-}
-__device__ __forceinline__ int block_max_i(int v, int* lds) {
-  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
-  __syncthreads();
-  int r = lds[0];
-  for (int i = 1; i < NW; ++i) r = max(r, lds[i]);
-  return r;
-}
-
-// Exclusive scan of one value per thread across the workgroup.
-__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* lds, int64_t* total) {
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int64_t inc = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    int64_t t = __shfl_up(inc, o, 64);
-    if (l >= o) inc += t;
-  }
-  __syncthreads();
-  if (l == 63) lds[w] = inc;
-  __syncthreads();
-  int64_t pre = 0, tot = 0;
-  for (int i = 0; i < NW; ++i) {
-    if (i < w) pre += lds[i];
-    tot += lds[i];
-  }
-  *total = tot;
-  return pre + inc - v;
-}
-
-// reference calc_jaccard (get_cliques.py:40-46), same f64 op order, no FMA.
-__device__ __forceinline__ double jaccard(double x, double y, double a, double b, double B,
-                                          double two_b2) {
-  const double xo = fmax((fmin(x, a) + B) - fmax(x, a), 0.0);
-  const double yo = fmax((fmin(y, b) + B) - fmax(y, b), 0.0);
-  const double inter = xo * yo;
-  return inter / (two_b2 - inter);
-}
 
 __device__ __forceinline__ int cell_of(const MgGrid& G, double x, double y) {
   if (G.ncell == 0 || !isfinite(x) || !isfinite(y)) return G.ncell;  // overflow bucket
@@ -420,13 +338,12 @@ __global__ __launch_bounds__(WG) void k4_stats(int k, const int32_t* __restrict_
     s.status = s.n_edges == 0 ? 1 : 0;
     s.target = -1;
     s.n_vert = 0;
+    s.clique_base = 0;
+    s.clique_cnt = 0;
     st[m] = s;
   }
 }
 
-__device__ __forceinline__ int pair_index(int j, int l, int k) {  // itertools.combinations
-  return j * (2 * k - j - 1) / 2 + (l - j - 1);
-}
 __device__ __forceinline__ uint64_t ins_pack(int pair, int la, int lb, int side) {
   return ((uint64_t)pair << 49) | ((uint64_t)la << 25) | ((uint64_t)lb << 1) | (uint64_t)side;
 }
@@ -547,119 +464,39 @@ struct Walk {
 };
 
 template <int K>
-__device__ __forceinline__ double median_of(double* v, int n) {
-  // numpy median (numpy/lib/_function_base_impl.py _median): middle value, or the mean of
-  // the two middle values ((a + b) / 2) for even n; NaN if any NaN.
-  for (int i = 0; i < n; ++i)
-    if (isnan(v[i])) return v[i];
-  for (int i = 1; i < n; ++i) {
-    const double t = v[i];
-    int j = i - 1;
-    while (j >= 0 && v[j] > t) { v[j + 1] = v[j]; --j; }
-    v[j + 1] = t;
-  }
-  if (n & 1) return v[n / 2];
-  return (v[n / 2 - 1] + v[n / 2]) / 2.0;
-}
-
-template <int K>
 __device__ void emit_clique(const CliqueArgs& A, Walk<K>& W) {
   const int64_t j = W.out++;
   const int m = W.m;
-  double s[K];
-#pragma unroll
-  for (int i = 0; i < K; ++i) s[i] = A.score[W.mem[i]];
-  const double conf = median_of<K>(s, K);
-  constexpr int NE = K * (K - 1) / 2;
-  double ej[NE > 0 ? NE : 1];
-  {
-    int t = 0;
-#pragma unroll
-    for (int a = 0; a < K; ++a)
-#pragma unroll
-      for (int b = a + 1; b < K; ++b) ej[t++] = W.ji[a][b];
-  }
-  const double med = median_of<K>(ej, NE);
-  const float conf32 = (float)conf;
-  const float w32 = (float)((double)conf32 * med);
-  // weighted degree: sum of JIs to the other members in increasing picker order
-  // (networkx DegreeView over adjacency insertion order, naive left-to-right f64 sum)
-  double deg[K];
+  double s[K], xs[K], ys[K];
+  int64_t ids[K];
+  uint64_t ins[K];
+  const int64_t idb = A.id_base[m] - (int64_t)A.box_off[m * A.k];
 #pragma unroll
   for (int i = 0; i < K; ++i) {
-    double d = 0.0;
-#pragma unroll
-    for (int q = 0; q < K; ++q) {
-      if (q == i) continue;
-      d = d + (q < i ? W.ji[q][i] : W.ji[i][q]);
-    }
-    deg[i] = d;
-  }
-  double dmax = deg[0];
-  int nmax = 1, arg = 0;
-#pragma unroll
-  for (int i = 1; i < K; ++i) {
-    if (deg[i] > dmax) { dmax = deg[i]; nmax = 1; arg = i; }
-    else if (deg[i] == dmax) ++nmax;
+    const int g = W.mem[i];
+    s[i] = A.score[g];
+    xs[i] = A.x[g];
+    ys[i] = A.y[g];
+    ids[i] = idb + g;
   }
   const bool multi = (A.flags & 2) != 0;
-  int8_t ord[K];
-  if (nmax > 1 || multi) {
-    if (2 * K < A.st[m].n_nodes) {
-      // CPython set(sorted(clique)) iteration order; insertion order is sorted (x, y, id)
-      int8_t srt[K];
+  const bool set_order = 2 * K < A.st[m].n_nodes;
+  if (!set_order) {
 #pragma unroll
-      for (int i = 0; i < K; ++i) srt[i] = (int8_t)i;
-      for (int i = 1; i < K; ++i) {
-        const int8_t t = srt[i];
-        const double tx = A.x[W.mem[t]], ty = A.y[W.mem[t]];
-        const int tg = W.mem[t];
-        int q = i - 1;
-        while (q >= 0) {
-          const int u = W.mem[srt[q]];
-          const double ux = A.x[u], uy = A.y[u];
-          const bool gt = (ux > tx) || (ux == tx && (uy > ty || (uy == ty && u > tg)));
-          if (!gt) break;
-          srt[q + 1] = srt[q];
-          --q;
-        }
-        srt[q + 1] = t;
-      }
-      uint64_t hs[K];
-      const int64_t idb = A.id_base[m] - (int64_t)A.box_off[m * A.k];
-      for (int i = 0; i < K; ++i) {
-        const int g = W.mem[srt[i]];
-        hs[i] = pyset::hash_node(A.x[g], A.y[g], idb + g);
-      }
-      int8_t so[K];
-      pyset::set_order(hs, K, so);
-      for (int i = 0; i < K; ++i) ord[i] = srt[so[i]];
-    } else {
-      // graph insertion order (FilterAtlas iterates the graph when 2k >= |G|)
-      unsigned long long kk[K];
-      for (int i = 0; i < K; ++i) { kk[i] = A.ins_key[W.mem[i]]; ord[i] = (int8_t)i; }
-      for (int i = 1; i < K; ++i) {
-        const int8_t t = ord[i];
-        int q = i - 1;
-        while (q >= 0 && kk[ord[q]] > kk[t]) { ord[q + 1] = ord[q]; --q; }
-        ord[q + 1] = t;
-      }
-    }
-    if (nmax > 1) {
-      for (int i = 0; i < K; ++i)
-        if (deg[ord[i]] == dmax) { arg = ord[i]; break; }
-    }
+    for (int i = 0; i < K; ++i) ins[i] = A.ins_key[W.mem[i]];
   }
-  A.w[j] = w32;
-  A.conf[j] = conf32;
-  A.consensus[j] = W.mem[arg];
+  Epi<K> e;
+  epilogue<K>(W.mem, W.ji, s, xs, ys, ids, set_order, ins, multi, e);
+  A.w[j] = e.w;
+  A.conf[j] = e.conf;
+  A.consensus[j] = W.mem[e.arg];
 #pragma unroll
   for (int i = 0; i < K; ++i) {
     A.members[j * K + i] = W.mem[i];
     A.in_clique[W.mem[i]] = 1;
   }
   if (multi) {
-    for (int i = 0; i < K; ++i) A.order[j * K + i] = (uint8_t)ord[i];
+    for (int i = 0; i < K; ++i) A.order[j * K + i] = (uint8_t)e.ord[i];
   }
 }
 
@@ -831,7 +668,50 @@ __global__ __launch_bounds__(WG) void k_mg_offsets(int n_mg, int k, const int32_
   mg_off[m] = coff[box_off[m * k]];
 }
 
+// ----------------------------------------------------------------------------- sub-batch
+// Gather the boxes of deferred micrographs into a compact sub-batch for this path.
+__global__ __launch_bounds__(WG) void k_gather(int k, const int32_t* __restrict__ sub_mg,
+                                               const int32_t* __restrict__ box_off,
+                                               const int32_t* __restrict__ sub_box_off,
+                                               const double* __restrict__ x,
+                                               const double* __restrict__ y,
+                                               const double* __restrict__ s, double* ox,
+                                               double* oy, double* os, int32_t* orig) {
+  const int mp = blockIdx.x, m = sub_mg[mp];
+  const int b0 = box_off[m * k], n = box_off[m * k + k] - b0, d0 = sub_box_off[mp * k];
+  for (int i = threadIdx.x; i < n; i += WG) {
+    ox[d0 + i] = x[b0 + i];
+    oy[d0 + i] = y[b0 + i];
+    os[d0 + i] = s[b0 + i];
+    orig[d0 + i] = b0 + i;
+  }
+}
+
+__global__ __launch_bounds__(WG) void k_remap(int64_t C, int k, const int32_t* __restrict__ orig,
+                                              int32_t* consensus, int32_t* members) {
+  const int64_t j = (int64_t)blockIdx.x * WG + threadIdx.x;
+  if (j >= C) return;
+  consensus[j] = orig[consensus[j]];
+  for (int i = 0; i < k; ++i) members[j * k + i] = orig[members[j * k + i]];
+}
+
 // ----------------------------------------------------------------------------- launchers
+void launch_gather(hipStream_t stream, int n_sub, int k, const int32_t* sub_mg,
+                   const int32_t* box_off, const int32_t* sub_box_off, const double* x,
+                   const double* y, const double* s, double* ox, double* oy, double* os,
+                   int32_t* orig) {
+  if (n_sub > 0)
+    hipLaunchKernelGGL(k_gather, dim3(n_sub), dim3(WG), 0, stream, k, sub_mg, box_off,
+                       sub_box_off, x, y, s, ox, oy, os, orig);
+}
+
+void launch_remap(hipStream_t stream, int64_t C, int k, const int32_t* orig, int32_t* consensus,
+                  int32_t* members) {
+  const int64_t nb = (C + WG - 1) / WG;
+  if (nb > 0)
+    hipLaunchKernelGGL(k_remap, dim3(nb), dim3(WG), 0, stream, C, k, orig, consensus, members);
+}
+
 #define RGC_LAUNCH(kern, grid, block, ...) \
   hipLaunchKernelGGL(kern, dim3(grid), dim3(block), 0, stream, __VA_ARGS__)
 

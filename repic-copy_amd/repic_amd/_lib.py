@@ -22,6 +22,7 @@ if not os.path.exists(LIB_PATH):
 lib = C.CDLL(LIB_PATH)
 
 F_GET_CC, F_MULTI_OUT, F_DEVICE_INPUTS, F_HOST_OUTPUTS, F_TIMING = 1, 2, 4, 8, 16
+F_MEMBERS, F_NO_FUSED = 32, 64
 OK, NO_EDGES, NO_CLIQUES = 0, 1, 2
 PARSE_OK, PARSE_INDEX, PARSE_VALUE, PARSE_ASSERT, PARSE_FALLBACK, PARSE_OSERROR = range(6)
 MAX_K = 8
@@ -42,7 +43,8 @@ class BatchIn(C.Structure):
 class BatchOut(C.Structure):
     _fields_ = [("n_boxes", C.c_int64), ("n_edges", C.c_int64), ("n_cliques", C.c_int64),
                 ("status", _i32p), ("cc_max", _i32p), ("cc_cnt", _i32p), ("n_nodes", _i32p),
-                ("n_vert", _i32p), ("n_edges_mg", _i64p), ("clique_off", _i64p),
+                ("n_vert", _i32p), ("n_edges_mg", _i64p), ("clique_base", _i64p),
+                ("clique_cnt", _i64p),
                 ("rows", C.c_void_p), ("w", C.c_void_p), ("conf", C.c_void_p),
                 ("consensus", C.c_void_p), ("members", C.c_void_p), ("order", C.c_void_p)]
 
@@ -202,7 +204,8 @@ class Result:
         self.n_nodes = a(bo.n_nodes, n_mg).astype(np.int32)
         self.n_vert = a(bo.n_vert, n_mg).astype(np.int32)
         self.n_edges_mg = a(bo.n_edges_mg, n_mg).astype(np.int64)
-        self.clique_off = a(bo.clique_off, n_mg + 1).astype(np.int64)
+        self.clique_base = a(bo.clique_base, n_mg).astype(np.int64)
+        self.clique_cnt = a(bo.clique_cnt, n_mg).astype(np.int64)
         C_ = int(self.n_cliques)
         if flags & F_HOST_OUTPUTS:
             def h(p, ct, n):
@@ -213,7 +216,8 @@ class Result:
             self.w = h(bo.w, C.c_float, C_)
             self.conf = h(bo.conf, C.c_float, C_)
             self.consensus = h(bo.consensus, C.c_int32, C_)
-            self.members = h(bo.members, C.c_int32, C_ * k).reshape(C_, k)
+            self.members = (h(bo.members, C.c_int32, C_ * k).reshape(C_, k)
+                            if (flags & (F_MULTI_OUT | F_MEMBERS)) else None)
             self.order = (h(bo.order, C.c_uint8, C_ * k).reshape(C_, k)
                           if (flags & F_MULTI_OUT) else None)
         else:

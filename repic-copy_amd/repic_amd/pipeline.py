@@ -55,9 +55,14 @@ class MgResult:
                  "consensus", "members", "order")
 
 
-def run_batch(ctx: _lib.Context, batch: Batch, get_cc=False, multi_out=False, timing=False):
+def run_batch(ctx: _lib.Context, batch: Batch, get_cc=False, multi_out=False, timing=False,
+              members=False, no_fused=False):
     """Run one packed batch on the device; returns list[MgResult] (batch-local box indices)."""
     flags = _lib.F_HOST_OUTPUTS
+    if members:
+        flags |= _lib.F_MEMBERS
+    if no_fused:
+        flags |= _lib.F_NO_FUSED
     if get_cc:
         flags |= _lib.F_GET_CC
     if multi_out:
@@ -72,12 +77,13 @@ def run_batch(ctx: _lib.Context, batch: Batch, get_cc=False, multi_out=False, ti
         q.status = int(r.status[m])
         q.cc_max, q.cc_cnt = int(r.cc_max[m]), int(r.cc_cnt[m])
         q.n_vert, q.n_edges = int(r.n_vert[m]), int(r.n_edges_mg[m])
-        c0, c1 = int(r.clique_off[m]), int(r.clique_off[m + 1])
+        c0 = int(r.clique_base[m])
+        c1 = c0 + int(r.clique_cnt[m])
         q.rows = r.rows[c0:c1].copy()
         q.w = r.w[c0:c1].copy()
         q.conf = r.conf[c0:c1].copy()
         q.consensus = r.consensus[c0:c1].copy()
-        q.members = r.members[c0:c1].copy()
+        q.members = r.members[c0:c1].copy() if r.members is not None else None
         q.order = r.order[c0:c1].copy() if r.order is not None else None
         out.append(q)
     return out

@@ -25,8 +25,12 @@ def _args(in_dir, out_dir, meta, **kw):
     return a
 
 
-def _run_case(name, tmp_path, **kw):
+def _run_case(name, tmp_path, no_fused=False, **kw):
+    from repic_amd import pipeline
     from repic_amd.commands import get_cliques
+    if no_fused:
+        orig = pipeline.run_batch
+        get_cliques.run_batch = lambda *a, **k_: orig(*a, no_fused=True, **k_)
     meta, data = load_case(name)
     in_dir = make_inputs(name, str(tmp_path))
     out_dir = os.path.join(str(tmp_path), "out")
@@ -35,6 +39,8 @@ def _run_case(name, tmp_path, **kw):
         get_cliques.main(_args(in_dir, out_dir, meta, **kw))
     except Exception as e:  # noqa: BLE001 - the exception class is part of the contract
         exc = e
+    finally:
+        get_cliques.run_batch = pipeline.run_batch
     if meta["exception"]:
         assert exc is not None and isinstance(exc, getattr(builtins, meta["exception"])), exc
     else:
@@ -46,6 +52,12 @@ def _run_case(name, tmp_path, **kw):
 @pytest.mark.parametrize("name", golden_cases())
 def test_gpu_matches_reference_golden(name, tmp_path):
     _run_case(name, tmp_path)
+
+
+@pytest.mark.parametrize("name", golden_cases())
+def test_gpu_multikernel_path_matches_reference_golden(name, tmp_path):
+    """The multi-kernel path (used for micrographs too large for the fused kernel's LDS)."""
+    _run_case(name, tmp_path, no_fused=True)
 
 
 @pytest.mark.parametrize("name", ["c1_10017", "syn_k3", "skips", "ties_getcc"])
@@ -71,9 +83,10 @@ def _canon(rows, w, conf, cons_xyid):
             np.asarray(conf)[perm].view(np.uint32), [cons_xyid[i] for i in perm])
 
 
-@pytest.mark.parametrize("cfg_name,n_mg,get_cc", [("C2", 24, False), ("C2", 8, True),
-                                                   ("C4", 6, False)])
-def test_gpu_matches_oracle_synthetic(cfg_name, n_mg, get_cc):
+@pytest.mark.parametrize("cfg_name,n_mg,get_cc,no_fused", [
+    ("C2", 24, False, False), ("C2", 8, True, False), ("C4", 6, False, False),
+    ("C2", 8, False, True), ("C3", 2, False, False), ("C3", 1, True, False)])
+def test_gpu_matches_oracle_synthetic(cfg_name, n_mg, get_cc, no_fused):
     from repic_amd import _lib, synth
     from repic_amd.pipeline import Batch, run_batch
     cfg = synth.SynthConfig(**synth.CONFIGS[cfg_name], seed=5, logit=(1,))
@@ -82,7 +95,7 @@ def test_gpu_matches_oracle_synthetic(cfg_name, n_mg, get_cc):
     mgs = [[(x, y, sigmoid(s) if s.min() < 0 else s) for (x, y, s) in mg] for mg in mgs]
     batch = Batch.pack(cfg.k, cfg.box, mgs)
     ctx = _lib.Context(0)
-    res = run_batch(ctx, batch, get_cc=get_cc)
+    res = run_batch(ctx, batch, get_cc=get_cc, no_fused=no_fused)
     methods = [f"picker{p}" for p in range(cfg.k)]
     for m, mg in enumerate(mgs):
         o = _oracle_mg(mg, cfg.box, methods, int(batch.id_base[m]), get_cc)
@@ -112,13 +125,17 @@ def test_gpu_full_c2_properties():
     batch = Batch.pack(cfg.k, cfg.box, synth.batch(cfg, 10000))
     ctx = _lib.Context(0)
     r = ctx.run(batch.n_mg, cfg.k, cfg.box, batch.box_off, batch.id_base, batch.x, batch.y,
-                batch.score, _lib.F_HOST_OUTPUTS)
+                batch.score, _lib.F_HOST_OUTPUTS | _lib.F_MEMBERS)
     assert (r.status == 0).all()
     C = int(r.n_cliques)
-    assert C == int(r.clique_off[-1]) and C > 10000 * 300
+    assert C == int(r.clique_cnt.sum()) and C > 10000 * 300
+    # micrograph ranges tile [0, C) without overlap
+    o = np.argsort(r.clique_base)
+    assert (r.clique_base[o][1:] == (r.clique_base + r.clique_cnt)[o][:-1]).all()
     mem = r.members.astype(np.int64)
-    # members: one box per picker, inside their micrograph
-    mg_of = np.searchsorted(batch.box_off[::cfg.k], mem[:, 0], side="right") - 1
+    # members: one box per picker, inside their micrograph (the one owning the range)
+    mg_of = np.repeat(o, r.clique_cnt[o])   # ranges tile [0, C) in base order
+    assert (np.searchsorted(batch.box_off[::cfg.k], mem[:, 0], side="right") - 1 == mg_of).all()
     for p in range(cfg.k):
         lo = batch.box_off[mg_of * cfg.k + p]
         hi = batch.box_off[mg_of * cfg.k + p + 1]
