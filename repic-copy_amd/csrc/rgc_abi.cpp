@@ -51,7 +51,7 @@ enum DevBufId {
   // outputs
   D_ROWS, D_W, D_CONF, D_CONS, D_MEMBERS, D_ORDER,
   // multi-kernel path (sub-batch)
-  D_SUBMG, D_SUBX, D_SUBY, D_SUBS, D_ORIG,
+  D_SUBMG, D_SUBX, D_SUBY, D_SUBS, D_ORIG, D_STAMPS,
   D_BOXOFF, D_CELLOFF, D_IDBASE, D_GRID, D_CELLSTART, D_SX, D_SY, D_SBOX, D_SPICK, D_SMG, D_BMG,
   D_BPICK, D_FWDCNT, D_FWDOFF, D_TILES, D_TOTAL, D_EDST, D_EJI, D_PARENT, D_HASEDGE, D_CSIZE,
   D_STAT, D_INSKEY, D_COMPMIN, D_CCOUNT, D_COFF, D_INCL, D_VLIST, D_VSORT, D_VROW, D_MGOFF,
@@ -68,9 +68,11 @@ struct Buf {
 };
 
 // Fused size classes: boxes per micrograph and forward-edge capacity per class.
+// (LDS bytes ~ 46 n + 2 ecap: class 1024 with ecap 3n fits 3 workgroups per CU, the top class
+// fills the 160 KiB of one CU)
 constexpr int N_CLASSES = 5;
-constexpr int CLASS_N[N_CLASSES] = {256, 512, 1024, 2048, 3200};
-inline int class_ecap(int nmax) { return 4 * nmax; }
+constexpr int CLASS_N[N_CLASSES] = {256, 512, 1024, 2048, 3000};
+constexpr int CLASS_E[N_CLASSES] = {4 * 256, 4 * 512, 3 * 1024, 4 * 2048, 4 * 3000};
 
 }  // namespace
 
@@ -87,6 +89,7 @@ struct rgc_ctx {
   std::vector<float> times;
   std::vector<const char*> time_names;
   int64_t cap_cliques = 0;   // capacity of the per-clique output arrays
+  std::vector<uint64_t> stamps;   // diagnostic build only
   // per-micrograph host outputs
   std::vector<int32_t> status, cc_max, cc_cnt, n_nodes, n_vert;
   std::vector<int64_t> n_edges_mg, clique_base, clique_cnt;
@@ -364,6 +367,8 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   std::vector<int32_t> cls_list[N_CLASSES];
   std::vector<int32_t> big;
   const bool no_fused = (flags & RGC_F_NO_FUSED) != 0;
+  for (int q = 0; q < N_CLASSES; ++q)
+    if (fused_lds_bytes(CLASS_N[q], CLASS_E[q]) > 160 * 1024) return fail("internal: LDS class");
   for (int m = 0; m < n_mg; ++m) {
     const int64_t nm = in->box_off[(int64_t)(m + 1) * k] - in->box_off[(int64_t)m * k];
     int cl = -1;
@@ -433,13 +438,21 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
       A.consensus = D<int32_t>(c, D_CONS);
       A.members = want_members ? D<int32_t>(c, D_MEMBERS) : nullptr;
       A.order = multi ? D<uint8_t>(c, D_ORDER) : nullptr;
+      A.stamps = nullptr;
+#ifdef RGC_STAMPS
+      TRY(ensure_dev(c, D_STAMPS, (size_t)n_fused * 16 * 8));
+      HIPCHK(hipMemsetAsync(D<void>(c, D_STAMPS), 0, (size_t)n_fused * 128, s));
+#endif
       int o = 0;
       for (int q = 0; q < N_CLASSES; ++q) {
         const int nb = (int)cls_list[q].size();
         if (!nb) continue;
         A.nmax = CLASS_N[q];
-        A.ecap = class_ecap(CLASS_N[q]);
+        A.ecap = CLASS_E[q];
         A.mg_list = D<int32_t>(c, D_MGLIST) + o;
+#ifdef RGC_STAMPS
+        A.stamps = D<unsigned long long>(c, D_STAMPS) + (size_t)o * 16;
+#endif
         TRY(mark(c, "k_fused"));
         if (launch_fused(s, nb, fused_lds_bytes(A.nmax, A.ecap), A) != 0)
           return fail("fused kernel launch failed");
@@ -452,6 +465,11 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
       HIPCHK(hipGetLastError());
       HIPCHK(hipStreamSynchronize(s));
       fused_total = (int64_t)H<unsigned long long>(c, H_TOTAL)[0];
+#ifdef RGC_STAMPS
+      c->stamps.resize((size_t)n_fused * 16);
+      HIPCHK(hipMemcpy(c->stamps.data(), D<void>(c, D_STAMPS), (size_t)n_fused * 128,
+                       hipMemcpyDeviceToHost));
+#endif
       if (fused_total <= c->cap_cliques) break;
       c->cap_cliques = fused_total + fused_total / 8 + 1024;   // grow and re-run once
       c->n_ev = 0;
@@ -635,6 +653,16 @@ int rgc_kernel_times(rgc_ctx* c, int max_n, float* ms, const char** names) {
 }
 
 uint64_t rgc_py_hash_node(double x, double y, int64_t id) { return pyset::hash_node(x, y, id); }
+
+#ifdef RGC_STAMPS
+// Diagnostic build only: s_memtime stamps (8 per fused workgroup, launch order) of the
+// last rgc_run.
+int64_t rgc_diag_stamps(rgc_ctx* c, uint64_t* out, int64_t max_n) {
+  const int64_t n = std::min<int64_t>(max_n, (int64_t)c->stamps.size());
+  if (out) std::memcpy(out, c->stamps.data(), n * 8);
+  return (int64_t)c->stamps.size();
+}
+#endif
 
 int rgc_py_set_order(const uint64_t* hashes, int n, int8_t* out) {
   if (n < 0 || n > 18) return fail("set_order supports 0..18 keys");

@@ -13,42 +13,47 @@ constexpr int WG = 256;
 constexpr int NW = WG / 64;
 
 // ----------------------------------------------------------------------------- block reductions
+template <int BS = WG>
 __device__ __forceinline__ double block_min(double v, double* lds) {
   for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
   __syncthreads();
   if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
   __syncthreads();
   double r = lds[0];
-  for (int i = 1; i < NW; ++i) r = fmin(r, lds[i]);
+  for (int i = 1; i < BS / 64; ++i) r = fmin(r, lds[i]);
   return r;
 }
+template <int BS = WG>
 __device__ __forceinline__ double block_max(double v, double* lds) {
   for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
   __syncthreads();
   if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
   __syncthreads();
   double r = lds[0];
-  for (int i = 1; i < NW; ++i) r = fmax(r, lds[i]);
+  for (int i = 1; i < BS / 64; ++i) r = fmax(r, lds[i]);
   return r;
 }
+template <int BS = WG>
 __device__ __forceinline__ int64_t block_sum64(int64_t v, int64_t* lds) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
   __syncthreads();
   int64_t r = 0;
-  for (int i = 0; i < NW; ++i) r += lds[i];
+  for (int i = 0; i < BS / 64; ++i) r += lds[i];
   return r;
 }
+template <int BS = WG>
 __device__ __forceinline__ int block_max_i(int v, int* lds) {
   for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
   __syncthreads();
   if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
   __syncthreads();
   int r = lds[0];
-  for (int i = 1; i < NW; ++i) r = max(r, lds[i]);
+  for (int i = 1; i < BS / 64; ++i) r = max(r, lds[i]);
   return r;
 }
+template <int BS = WG>
 __device__ __forceinline__ uint64_t block_min_u64(uint64_t v, uint64_t* lds) {
   for (int o = 32; o > 0; o >>= 1) {
     const uint64_t t = __shfl_xor(v, o, 64);
@@ -58,11 +63,12 @@ __device__ __forceinline__ uint64_t block_min_u64(uint64_t v, uint64_t* lds) {
   if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
   __syncthreads();
   uint64_t r = lds[0];
-  for (int i = 1; i < NW; ++i) r = lds[i] < r ? lds[i] : r;
+  for (int i = 1; i < BS / 64; ++i) r = lds[i] < r ? lds[i] : r;
   return r;
 }
 
 // Exclusive scan of one value per thread across the workgroup.
+template <int BS = WG>
 __device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* lds, int64_t* total) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   int64_t inc = v;
@@ -74,7 +80,7 @@ __device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* lds, int6
   if (l == 63) lds[w] = inc;
   __syncthreads();
   int64_t pre = 0, tot = 0;
-  for (int i = 0; i < NW; ++i) {
+  for (int i = 0; i < BS / 64; ++i) {
     if (i < w) pre += lds[i];
     tot += lds[i];
   }
@@ -84,16 +90,35 @@ __device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* lds, int6
 
 // In-place exclusive scan of a[0..n) (LDS, u32), each thread a contiguous chunk.
 // Returns the total.  Ends with a barrier.
+template <int BS = WG>
 __device__ __forceinline__ int64_t block_scan_array(uint32_t* a, int n, int64_t* lds) {
-  const int per = (n + WG - 1) / WG;
+  const int per = (n + BS - 1) / BS;
   const int c0 = min((int)threadIdx.x * per, n), c1 = min(c0 + per, n);
   int64_t s = 0;
   for (int c = c0; c < c1; ++c) s += a[c];
   int64_t tot;
-  int64_t pre = block_excl_scan(s, lds, &tot);
+  int64_t pre = block_excl_scan<BS>(s, lds, &tot);
   for (int c = c0; c < c1; ++c) {
     const uint32_t v = a[c];
     a[c] = (uint32_t)pre;
+    pre += v;
+  }
+  __syncthreads();
+  return tot;
+}
+
+// In-place exclusive scan of a[0..n) (LDS, u16 values whose total fits 16 bits).
+template <int BS = WG>
+__device__ __forceinline__ int64_t block_scan_u16(uint16_t* a, int n, int64_t* lds) {
+  const int per = (n + BS - 1) / BS;
+  const int c0 = min((int)threadIdx.x * per, n), c1 = min(c0 + per, n);
+  int64_t s = 0;
+  for (int c = c0; c < c1; ++c) s += a[c];
+  int64_t tot;
+  int64_t pre = block_excl_scan<BS>(s, lds, &tot);
+  for (int c = c0; c < c1; ++c) {
+    const uint16_t v = a[c];
+    a[c] = (uint16_t)pre;
     pre += v;
   }
   __syncthreads();

@@ -24,11 +24,14 @@
 
 namespace rgc {
 
+constexpr int FWG = 512;            // fused-kernel workgroup: 8 waves per micrograph
+constexpr int FNW = FWG / 64;
+
 struct FusedHdr {
-  double redd[NW];
-  int64_t red64[NW];
-  uint64_t redu[NW];
-  int redi[NW];
+  double redd[FNW];
+  int64_t red64[FNW];
+  uint64_t redu[FNW];
+  int redi[FNW];
   double minx, miny, cell;
   int gx, gy, ncell;
   int E, nodes, cc_cnt, cc_max, target, V, status;
@@ -39,15 +42,17 @@ __host__ __device__ inline FusedLayout fused_layout(int nmax, int ecap) {
   FusedLayout L;
   auto al = [](int v) { return (v + 15) & ~15; };
   int o = al((int)sizeof(FusedHdr));
-  L.off_xs = o; o += al(8 * nmax);
-  L.off_ys = o; o += al(8 * nmax);
-  L.off_cstart = o; o += al(4 * (nmax + 4));
+  L.off_sxy = o; o += al(16 * nmax);          // (x, y) in cell-sorted order
+  L.off_cstart = o; o += al(2 * (4 * nmax + 8));   // u16 cell starts, <= 4n + 1 cells
   L.off_cnt = o; o += al(4 * (nmax + 4));
   L.off_fwd = o; o += al(4 * (nmax + 4));
   L.off_parent = o; o += al(4 * (nmax + 4));
-  L.off_citems = o; o += al(2 * nmax);
+  L.off_citems = o; o += al(2 * nmax);        // sorted position -> local box index
+  L.off_pos = o; o += al(2 * nmax);           // local box index -> sorted position
+  L.off_scell = o; o += al(2 * nmax);         // sorted position -> cell
   L.off_vrank = o; o += al(2 * nmax);
-  L.off_flags = o; o += al(nmax);
+  L.off_flags = o; o += al(nmax);             // by local index
+  L.off_smark = o; o += al(nmax);             // clique-vertex mark by sorted position
   L.off_dst = o; o += al(2 * ecap);
   L.total = o;
   return L;
@@ -56,21 +61,33 @@ __host__ __device__ inline FusedLayout fused_layout(int nmax, int ecap) {
 int fused_lds_bytes(int nmax, int ecap) { return fused_layout(nmax, ecap).total; }
 
 struct FShared {
-  double* xs;
-  double* ys;
-  uint32_t* cstart;
+  double2* sxy;     // cell-sorted coordinates
+  uint16_t* cstart;
   uint32_t* cnt;
   uint32_t* fwd;
   uint32_t* parent;
   uint16_t* citems;
+  uint16_t* pos;
+  uint16_t* scell;
   uint16_t* vrank;
-  uint8_t* flags;   // 0: no edge, 1: graph node, 3: clique vertex
+  uint8_t* flags;   // by local index: 0 no edge, 1 graph node, 3 clique vertex
+  uint8_t* smark;   // by sorted position: 1 clique vertex
   uint16_t* dst;
 };
 
 template <int K>
 struct FCtx {
-  const FusedArgs* A;
+  // copies of the kernel arguments (taking the address of the kernarg struct would move it
+  // to scratch)
+  double B, two_b2;
+  int flags;
+  const double* score;
+  int32_t* rows;
+  float* w;
+  float* conf;
+  int32_t* consensus;
+  int32_t* members;
+  uint8_t* order;
   FShared S;
   int pb[K + 1];     // picker bounds (local box indices)
   int m, b0, n;
@@ -103,6 +120,21 @@ __device__ __forceinline__ int picker_of(const int (&pb)[K + 1], int i) {
   for (int q = 1; q < K; ++q) p += (i >= pb[q]);
   return p;
 }
+// first box index after box i's picker (unrolled select, no dynamic indexing)
+template <int K>
+__device__ __forceinline__ int picker_end(const int (&pb)[K + 1], int i) {
+  int e = pb[K];
+#pragma unroll
+  for (int q = K - 1; q >= 1; --q) e = (i < pb[q]) ? pb[q] : e;
+  return e;
+}
+template <int K>
+__device__ __forceinline__ int picker_begin(const int (&pb)[K + 1], int p) {
+  int b = pb[0];
+#pragma unroll
+  for (int q = 1; q < K; ++q) b = (p == q) ? pb[q] : b;
+  return b;
+}
 
 __device__ __forceinline__ int lb16(const uint16_t* a, int lo, int hi, int v) {
   while (lo < hi) {
@@ -129,39 +161,40 @@ __device__ __forceinline__ int cell_xm(const FusedHdr& H, double x, double y, in
 template <int K>
 __device__ uint64_t ins_key(const FCtx<K>& c, int u) {
   const int pu = picker_of<K>(c.pb, u);
-  const int lu = u - c.pb[pu];
-  for (int a = 0; a < c.pb[pu]; ++a) {
+  const int bu = picker_begin<K>(c.pb, pu);
+  const int lu = u - bu;
+  for (int a = 0; a < bu; ++a) {
     if (contains16(c.S.dst, c.S.fwd[a], c.S.fwd[a + 1], u)) {
       const int qa = picker_of<K>(c.pb, a);
-      return ((uint64_t)pair_index(qa, pu, K) << 49) | ((uint64_t)(a - c.pb[qa]) << 25) |
-             ((uint64_t)lu << 1) | 1ULL;
+      return ((uint64_t)pair_index(qa, pu, K) << 49) |
+             ((uint64_t)(a - picker_begin<K>(c.pb, qa)) << 25) | ((uint64_t)lu << 1) | 1ULL;
     }
   }
   const int d0 = c.S.dst[c.S.fwd[u]];
   const int pd = picker_of<K>(c.pb, d0);
   return ((uint64_t)pair_index(pu, pd, K) << 49) | ((uint64_t)lu << 25) |
-         ((uint64_t)(d0 - c.pb[pd]) << 1);
+         ((uint64_t)(d0 - picker_begin<K>(c.pb, pd)) << 1);
 }
 
 template <int K>
 __device__ void fused_emit(FCtx<K>& c, const int (&mem)[K]) {
-  const FusedArgs& A = *c.A;
   const int64_t j = c.out++;
   double ji[K][K], s[K], xs[K], ys[K];
   int64_t ids[K];
   uint64_t ins[K];
 #pragma unroll
   for (int i = 0; i < K; ++i) {
-    xs[i] = c.S.xs[mem[i]];
-    ys[i] = c.S.ys[mem[i]];
-    s[i] = A.score[c.b0 + mem[i]];
+    const double2 xy = c.S.sxy[c.S.pos[mem[i]]];
+    xs[i] = xy.x;
+    ys[i] = xy.y;
+    s[i] = c.score[c.b0 + mem[i]];
     ids[i] = c.idb + mem[i];
   }
 #pragma unroll
   for (int a = 0; a < K; ++a)
 #pragma unroll
-    for (int b = a + 1; b < K; ++b) ji[a][b] = jaccard(xs[a], ys[a], xs[b], ys[b], A.B, A.two_b2);
-  const bool multi = (A.flags & 2) != 0;
+    for (int b = a + 1; b < K; ++b) ji[a][b] = jaccard(xs[a], ys[a], xs[b], ys[b], c.B, c.two_b2);
+  const bool multi = (c.flags & 2) != 0;
   if (!c.set_order) {
     for (int i = 0; i < K; ++i) ins[i] = ins_key<K>(c, mem[i]);
   }
@@ -179,17 +212,20 @@ __device__ void fused_emit(FCtx<K>& c, const int (&mem)[K]) {
       r[q + 1] = max(a, b);
     }
 #pragma unroll
-  for (int i = 0; i < K; ++i) A.rows[j * K + i] = r[i];
-  A.w[j] = e.w;
-  A.conf[j] = e.conf;
-  A.consensus[j] = c.b0 + mem[e.arg];
-  if (A.flags & (2 | 32)) {
+  for (int i = 0; i < K; ++i) c.rows[j * K + i] = r[i];
+  c.w[j] = e.w;
+  c.conf[j] = e.conf;
+  int cons = mem[0];
 #pragma unroll
-    for (int i = 0; i < K; ++i) A.members[j * K + i] = c.b0 + mem[i];
+  for (int i = 1; i < K; ++i) cons = (e.arg == i) ? mem[i] : cons;
+  c.consensus[j] = c.b0 + cons;
+  if (c.flags & (2 | 32)) {
+#pragma unroll
+    for (int i = 0; i < K; ++i) c.members[j * K + i] = c.b0 + mem[i];
   }
   if (multi) {
 #pragma unroll
-    for (int i = 0; i < K; ++i) A.order[j * K + i] = (uint8_t)e.ord[i];
+    for (int i = 0; i < K; ++i) c.order[j * K + i] = (uint8_t)e.ord[i];
   }
 }
 
@@ -223,31 +259,151 @@ struct FLevel<K, K, FILL> {
     } else {
       ++c.count;
 #pragma unroll
-      for (int i = 0; i < K; ++i) c.S.flags[mem[i]] = 3;
+      for (int i = 0; i < K; ++i) {
+        c.S.flags[mem[i]] = 3;
+        c.S.smark[c.S.pos[mem[i]]] = 1;
+      }
     }
   }
 };
 
+// 3x3 stencil of a box (sorted position ts) as three column ranges of sorted positions.
+struct Stencil {
+  int i, pe, lo0, L0, lo1, L01, lo2, L;
+  double2 a;
+};
+
 template <int K>
-__global__ __launch_bounds__(WG) void k_fused(FusedArgs A) {
+__device__ __forceinline__ void stencil_setup(Stencil& st, int ts, const FShared& S,
+                                              const FusedHdr& H, const int (&pb)[K + 1]) {
+  const int q = S.scell[ts];
+  st.i = S.citems[ts];
+  st.pe = picker_end<K>(pb, st.i);
+  st.a = S.sxy[ts];
+  st.lo0 = st.lo1 = st.lo2 = 0;
+  st.L0 = st.L01 = st.L = 0;
+  if (q >= H.ncell) return;
+  const int gy = H.gy;
+  const int cx = q / gy, cy = q - cx * gy;
+  const int y0 = max(cy - 1, 0), y1 = min(cy + 1, gy - 1);
+  int l0 = 0, h0 = 0, l1, h1, l2 = 0, h2 = 0;
+  if (cx > 0) { l0 = S.cstart[(cx - 1) * gy + y0]; h0 = S.cstart[(cx - 1) * gy + y1 + 1]; }
+  l1 = S.cstart[cx * gy + y0];
+  h1 = S.cstart[cx * gy + y1 + 1];
+  if (cx + 1 < H.gx) { l2 = S.cstart[(cx + 1) * gy + y0]; h2 = S.cstart[(cx + 1) * gy + y1 + 1]; }
+  st.lo0 = l0; st.lo1 = l1; st.lo2 = l2;
+  st.L0 = h0 - l0;
+  st.L01 = st.L0 + (h1 - l1);
+  st.L = st.L01 + (h2 - l2);
+}
+
+__device__ __forceinline__ bool edge_test(double2 a, double2 b, double B, double two_b2,
+                                          double i_lo, double i_hi) {
+  // same values as np.min/np.max on finite coordinates (no NaN canonicalisation)
+  const bool lx = a.x < b.x, ly = a.y < b.y;
+  double xo = ((lx ? a.x : b.x) + B) - (lx ? b.x : a.x);
+  xo = xo > 0.0 ? xo : 0.0;
+  if (xo * B < i_lo) return false;                           // I <= xo * B
+  double yo = ((ly ? a.y : b.y) + B) - (ly ? b.y : a.y);
+  yo = yo > 0.0 ? yo : 0.0;
+  const double inter = xo * yo;
+  if (inter > i_hi) return true;
+  if (inter < i_lo) return false;
+  return inter / (two_b2 - inter) > 0.3;                      // reference quotient
+}
+
+// Walk work items [w0, w1) (a contiguous chunk of the flattened (box, candidate) list).
+// FILL = 0: JI test, set the item's bit, count the edge for the owning box.
+// FILL = 1: replay the bits (or re-test when the bitmap did not fit) and append targets.
+template <int K, int FILL>
+__device__ __forceinline__ void walk_items(const FShared& S, const FusedHdr& H,
+                                           const int (&pb)[K + 1], const uint32_t* woff, int n,
+                                           int w0, int w1, uint32_t* ebits, bool use_bits,
+                                           double B, double two_b2, double i_lo, double i_hi) {
+  if (w0 >= w1) return;
+  int lo = 0, hi = n;                     // last ts with woff[ts] <= w0
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((int)woff[mid] <= w0) lo = mid; else hi = mid - 1;
+  }
+  int ts = lo;
+  Stencil st;
+  stencil_setup<K>(st, ts, S, H, pb);
+  int kk = w0 - (int)woff[ts];
+  for (int w = w0; w < w1; ++w, ++kk) {
+    while (kk >= st.L) {
+      ++ts;
+      kk = 0;
+      stencil_setup<K>(st, ts, S, H, pb);
+    }
+    const int t = kk < st.L0 ? st.lo0 + kk
+                             : (kk < st.L01 ? st.lo1 + (kk - st.L0) : st.lo2 + (kk - st.L01));
+    const int j = S.citems[t];
+    if (j < st.pe) continue;
+    if (FILL == 0) {
+      if (edge_test(st.a, S.sxy[t], B, two_b2, i_lo, i_hi)) {
+        if (use_bits) atomicOr(&ebits[w >> 5], 1u << (w & 31));
+        atomicAdd(&S.fwd[st.i], 1u);
+      }
+    } else {
+      const bool e = use_bits ? ((ebits[w >> 5] >> (w & 31)) & 1u)
+                              : edge_test(st.a, S.sxy[t], B, two_b2, i_lo, i_hi);
+      if (e) S.dst[atomicAdd(&S.cnt[st.i], 1u)] = (uint16_t)j;
+    }
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   FusedHdr& H = *reinterpret_cast<FusedHdr*>(smem);
   const FusedLayout L = fused_layout(A.nmax, A.ecap);
   FShared S;
-  S.xs = reinterpret_cast<double*>(smem + L.off_xs);
-  S.ys = reinterpret_cast<double*>(smem + L.off_ys);
-  S.cstart = reinterpret_cast<uint32_t*>(smem + L.off_cstart);
+  S.sxy = reinterpret_cast<double2*>(smem + L.off_sxy);
+  S.cstart = reinterpret_cast<uint16_t*>(smem + L.off_cstart);
   S.cnt = reinterpret_cast<uint32_t*>(smem + L.off_cnt);
   S.fwd = reinterpret_cast<uint32_t*>(smem + L.off_fwd);
   S.parent = reinterpret_cast<uint32_t*>(smem + L.off_parent);
   S.citems = reinterpret_cast<uint16_t*>(smem + L.off_citems);
+  S.pos = reinterpret_cast<uint16_t*>(smem + L.off_pos);
+  S.scell = reinterpret_cast<uint16_t*>(smem + L.off_scell);
   S.vrank = reinterpret_cast<uint16_t*>(smem + L.off_vrank);
   S.flags = reinterpret_cast<uint8_t*>(smem + L.off_flags);
+  S.smark = reinterpret_cast<uint8_t*>(smem + L.off_smark);
   S.dst = reinterpret_cast<uint16_t*>(smem + L.off_dst);
   const int tid = threadIdx.x;
   const int m = A.mg_list[blockIdx.x];
+#ifdef RGC_STAMPS
+  // diagnostic build only: per-phase s_memtime stamps of thread 0 (never in the product .so)
+#define STAMP(i)                                                                            \
+  do {                                                                                      \
+    __syncthreads();                                                                        \
+    if (tid == 0) A.stamps[(int64_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime();   \
+  } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
+#ifdef RGC_STOP_AFTER
+  // ablation build only: stop after phase RGC_STOP_AFTER (outputs incomplete)
+#define STOP_AFTER(ph)                            \
+  do {                                            \
+    if ((ph) == RGC_STOP_AFTER) {                 \
+      if (tid == 0) A.st[m] = MgStat{};           \
+      return;                                     \
+    }                                             \
+  } while (0)
+#else
+#define STOP_AFTER(ph) \
+  do {                 \
+  } while (0)
+#endif
+  STAMP(0);
   FCtx<K> c;
-  c.A = &A;
+  c.B = A.B; c.two_b2 = A.two_b2; c.flags = A.flags; c.score = A.score;
+  c.rows = A.rows; c.w = A.w; c.conf = A.conf; c.consensus = A.consensus;
+  c.members = A.members; c.order = A.order;
   c.S = S;
   c.m = m;
   c.b0 = A.box_off[m * K];
@@ -259,21 +415,23 @@ __global__ __launch_bounds__(WG) void k_fused(FusedArgs A) {
 
   // ---- P0: load coordinates, bounding box
   double mnx = INFINITY, mny = INFINITY, mxx = -INFINITY, mxy = -INFINITY;
-  for (int i = tid; i < n; i += WG) {
+  for (int i = tid; i < n; i += FWG) {
     const double xv = A.x[b0 + i], yv = A.y[b0 + i];
-    S.xs[i] = xv;
-    S.ys[i] = yv;
     if (isfinite(xv) && isfinite(yv)) {
       mnx = fmin(mnx, xv); mxx = fmax(mxx, xv);
       mny = fmin(mny, yv); mxy = fmax(mxy, yv);
     }
   }
-  mnx = block_min(mnx, H.redd);
-  mny = block_min(mny, H.redd);
-  mxx = block_max(mxx, H.redd);
-  mxy = block_max(mxy, H.redd);
+  mnx = block_min<FWG>(mnx, H.redd);
+  mny = block_min<FWG>(mny, H.redd);
+  mxx = block_max<FWG>(mxx, H.redd);
+  mxy = block_max<FWG>(mxy, H.redd);
 
-  // ---- P1: grid (x-major cells, side >= box_size, at most n + 1 cells)
+  STOP_AFTER(0);
+  STAMP(1);
+  // ---- P1: grid (x-major cells, at most 4n + 1 cells and n + 1 columns).  JI > 0.3 implies
+  // I > (6/13) B^2 and so |dx|, |dy| < (7/13) B = 0.5385 B: cells of side 0.54 B keep every
+  // edge inside the 3x3 stencil while the stencil area is 3.4x smaller than with side B.
   if (tid == 0) {
     H.minx = mnx; H.miny = mny; H.cell = A.B; H.gx = 0; H.gy = 0; H.ncell = 0;
     H.status = 0; H.C = 0; H.base = 0; H.V = 0; H.target = -1;
@@ -282,10 +440,13 @@ __global__ __launch_bounds__(WG) void k_fused(FusedArgs A) {
       if (!(ex < 0x1p40 && ey < 0x1p40)) {
         H.cell = INFINITY; H.gx = 1; H.gy = 1;
       } else {
-        double cl = A.B;
+        double cl = 0.54 * A.B;
         for (;;) {
           const double fx = floor(ex / cl) + 1.0, fy = floor(ey / cl) + 1.0;
-          if (fx * fy <= (double)(n + 1)) { H.gx = (int)fx; H.gy = (int)fy; break; }
+          if (fx * fy <= (double)(4 * n + 1) && fx <= (double)(n + 1)) {
+            H.gx = (int)fx; H.gy = (int)fy;
+            break;
+          }
           cl *= 2.0;
         }
         H.cell = cl;
@@ -295,73 +456,101 @@ __global__ __launch_bounds__(WG) void k_fused(FusedArgs A) {
   }
   __syncthreads();
   const int nc = H.ncell;
-  for (int q = tid; q <= nc; q += WG) S.cnt[q] = 0;
+  // counting sort by cell with packed u16 counters (two cells per LDS word)
+  uint32_t* cw = reinterpret_cast<uint32_t*>(S.cstart);
+  for (int q = tid; q <= (nc + 2) / 2; q += FWG) cw[q] = 0;
   __syncthreads();
-  for (int i = tid; i < n; i += WG) {
+  for (int i = tid; i < n; i += FWG) {
     int cx, cy;
-    atomicAdd(&S.cnt[cell_xm(H, S.xs[i], S.ys[i], &cx, &cy)], 1u);
+    const int q = cell_xm(H, A.x[b0 + i], A.y[b0 + i], &cx, &cy);
+    atomicAdd(&cw[q >> 1], 1u << (16 * (q & 1)));
   }
   __syncthreads();
-  for (int q = tid; q <= nc; q += WG) S.cstart[q] = S.cnt[q];
-  __syncthreads();
-  block_scan_array(S.cstart, nc + 1, H.red64);
-  if (tid == 0) S.cstart[nc + 1] = n;
-  for (int i = tid; i < n; i += WG) {
+  block_scan_u16<FWG>(S.cstart, nc + 1, H.red64);
+  for (int i = tid; i < n; i += FWG) {
     int cx, cy;
-    const int q = cell_xm(H, S.xs[i], S.ys[i], &cx, &cy);
-    const uint32_t old = atomicSub(&S.cnt[q], 1u);
-    S.citems[S.cstart[q] + old - 1] = (uint16_t)i;
+    const double xv = A.x[b0 + i], yv = A.y[b0 + i];
+    const int q = cell_xm(H, xv, yv, &cx, &cy);
+    const int sh = 16 * (q & 1);
+    const int t = (atomicAdd(&cw[q >> 1], 1u << sh) >> sh) & 0xFFFF;
+    S.citems[t] = (uint16_t)i;
+    S.pos[i] = (uint16_t)t;
+    S.scell[t] = (uint16_t)q;
+    S.sxy[t] = make_double2(xv, yv);
   }
+  __syncthreads();
+  // the cursors now hold cell ends: rebuild the starts from the sorted cell ids
+  for (int t = tid; t < n; t += FWG) {
+    const int q = S.scell[t];
+    const int qp = t ? (int)S.scell[t - 1] : -1;
+    for (int qq = qp + 1; qq <= q; ++qq) S.cstart[qq] = (uint16_t)t;
+    if (t == n - 1)
+      for (int qq = q + 1; qq <= nc + 1; ++qq) S.cstart[qq] = (uint16_t)n;
+  }
+  if (n == 0 && tid == 0)
+    for (int qq = 0; qq <= nc + 1; ++qq) S.cstart[qq] = 0;
   __syncthreads();
 
-  // ---- P2: Jaccard pairs (forward edges to higher pickers), count -> scan -> fill
+  STOP_AFTER(1);
+  STAMP(2);
+  // ---- P2: Jaccard pairs (forward edges to higher pickers).
+  // Work items = (box, stencil candidate).  Per-box item counts are scanned and every lane
+  // takes an equal contiguous chunk of items, so no lane waits on a long candidate list of
+  // its neighbour.  The count pass records one bit per item; the fill pass replays the bits.
   const double B = A.B, two_b2 = A.two_b2;
-  for (int pass = 0; pass < 2; ++pass) {
-    for (int i = tid; i < n; i += WG) {
-      int cx = 0, cy = 0;
-      const double xa = S.xs[i], ya = S.ys[i];
-      const int q = cell_xm(H, xa, ya, &cx, &cy);
-      int cntv = 0;
-      const int base = pass ? (int)S.fwd[i] : 0;
-      if (q < nc) {
-        const int pe = c.pb[picker_of<K>(c.pb, i) + 1];
-        const int y0 = max(cy - 1, 0), y1 = min(cy + 1, H.gy - 1);
-        for (int col = max(cx - 1, 0); col <= min(cx + 1, H.gx - 1); ++col) {
-          const int lo = S.cstart[col * H.gy + y0], hi = S.cstart[col * H.gy + y1 + 1];
-          for (int t = lo; t < hi; ++t) {
-            const int j = S.citems[t];
-            if (j < pe) continue;
-            double ji;
-            if (is_edge(xa, ya, S.xs[j], S.ys[j], B, two_b2, &ji)) {
-              if (pass) S.dst[base + cntv] = (uint16_t)j;
-              ++cntv;
-            }
-          }
-        }
-      }
-      if (!pass) {
-        S.fwd[i] = cntv;
-      } else {
-        for (int a = base + 1; a < base + cntv; ++a) {
-          const uint16_t key = S.dst[a];
-          int b = a - 1;
-          while (b >= base && S.dst[b] > key) { S.dst[b + 1] = S.dst[b]; --b; }
-          S.dst[b + 1] = key;
-        }
+  // JI > 0.3  <=>  I > (6/13) B^2 exactly; decide without the division unless I lies within a
+  // 2^-40 relative band of the threshold, where the reference's f64 quotient is evaluated.
+  // Outside the band the quotient's two roundings (< 3e-16 relative) cannot cross 0.3 (the
+  // band moves the quotient by >= 1.1e-12 relative), so the decision is the reference's.
+  const double t_star = 0.6 * B * B / 1.3;
+  const double i_lo = t_star * (1.0 - 0x1p-40), i_hi = t_star * (1.0 + 0x1p-40);
+  uint32_t* woff = S.parent;                                   // dead until P3
+  uint32_t* ebits = reinterpret_cast<uint32_t*>(S.vrank);     // dead until P5: 16 bits / box
+  for (int ts = tid; ts < n; ts += FWG) {
+    Stencil st;
+    stencil_setup<K>(st, ts, S, H, c.pb);
+    woff[ts] = st.L;
+  }
+  for (int i = tid; i < n; i += FWG) S.fwd[i] = 0;
+  __syncthreads();
+  const int W = (int)block_scan_array<FWG>(woff, n, H.red64);
+  STAMP(3);
+  if (tid == 0) woff[n] = W;
+  const bool use_bits = W <= 16 * n - 64;   // bitmap fits the vrank region
+  if (use_bits)
+    for (int q = tid; q < (W + 31) / 32; q += FWG) ebits[q] = 0;
+  __syncthreads();
+  const int chunk = (W + FWG - 1) / FWG;
+  const int w0 = min(W, tid * chunk), w1 = min(W, w0 + chunk);
+  // count pass
+  walk_items<K, 0>(S, H, c.pb, woff, n, w0, w1, ebits, use_bits, B, two_b2, i_lo, i_hi);
+  __syncthreads();
+  STAMP(4);
+  const int64_t E = block_scan_array<FWG>(S.fwd, n, H.red64);
+  if (tid == 0) {
+    S.fwd[n] = (uint32_t)E;
+    H.E = (int)E;
+    if (E == 0) H.status = RGC_ST_NO_EDGES;
+    else if (E > A.ecap) H.status = RGC_ST_DEFER;
+  }
+  for (int i = tid; i < n; i += FWG) S.cnt[i] = S.fwd[i];
+  __syncthreads();
+  STAMP(5);
+  if (H.status == 0) {
+    // fill pass, then sort every forward list by target (picker-major = id order)
+    walk_items<K, 1>(S, H, c.pb, woff, n, w0, w1, ebits, use_bits, B, two_b2, i_lo, i_hi);
+    __syncthreads();
+    STAMP(6);
+    for (int i = tid; i < n; i += FWG) {
+      const int base = S.fwd[i], end = S.fwd[i + 1];
+      for (int a = base + 1; a < end; ++a) {
+        const uint16_t key = S.dst[a];
+        int b = a - 1;
+        while (b >= base && S.dst[b] > key) { S.dst[b + 1] = S.dst[b]; --b; }
+        S.dst[b + 1] = key;
       }
     }
     __syncthreads();
-    if (!pass) {
-      const int64_t E = block_scan_array(S.fwd, n, H.red64);
-      if (tid == 0) {
-        S.fwd[n] = (uint32_t)E;
-        H.E = (int)E;
-        if (E == 0) H.status = RGC_ST_NO_EDGES;
-        else if (E > A.ecap) H.status = RGC_ST_DEFER;
-      }
-      __syncthreads();
-      if (H.status != 0) break;
-    }
   }
   if (H.status != 0) {
     if (tid == 0) {
@@ -374,10 +563,17 @@ __global__ __launch_bounds__(WG) void k_fused(FusedArgs A) {
     return;
   }
 
+  STOP_AFTER(2);
+  STAMP(7);
   // ---- P3: connected components (union-find in LDS)
-  for (int i = tid; i < n; i += WG) { S.parent[i] = i; S.flags[i] = 0; S.cnt[i] = 0; }
+  for (int i = tid; i < n; i += FWG) {
+    S.parent[i] = i;
+    S.flags[i] = 0;
+    S.smark[i] = 0;
+    S.cnt[i] = 0;
+  }
   __syncthreads();
-  for (int i = tid; i < n; i += WG) {
+  for (int i = tid; i < n; i += FWG) {
     const int e0 = S.fwd[i], e1 = S.fwd[i + 1];
     if (e0 == e1) continue;
     S.flags[i] = 1;
@@ -395,7 +591,7 @@ __global__ __launch_bounds__(WG) void k_fused(FusedArgs A) {
     }
   }
   __syncthreads();
-  for (int i = tid; i < n; i += WG) {
+  for (int i = tid; i < n; i += FWG) {
     if (!S.flags[i]) continue;
     const uint32_t r = uf_find_lds(S.parent, i);
     lds_st(S.parent + i, r);
@@ -405,15 +601,15 @@ __global__ __launch_bounds__(WG) void k_fused(FusedArgs A) {
   {
     int64_t nodes = 0, roots = 0;
     int mx = 0;
-    for (int i = tid; i < n; i += WG) {
+    for (int i = tid; i < n; i += FWG) {
       if (S.flags[i]) {
         ++nodes;
         if (S.parent[i] == (uint32_t)i) { ++roots; mx = max(mx, (int)S.cnt[i]); }
       }
     }
-    nodes = block_sum64(nodes, H.red64);
-    roots = block_sum64(roots, H.red64);
-    mx = block_max_i(mx, H.redi);
+    nodes = block_sum64<FWG>(nodes, H.red64);
+    roots = block_sum64<FWG>(roots, H.red64);
+    mx = block_max_i<FWG>(mx, H.redi);
     if (tid == 0) { H.nodes = (int)nodes; H.cc_cnt = (int)roots; H.cc_max = mx; }
   }
   const bool get_cc = (A.flags & 1) != 0;
@@ -421,7 +617,7 @@ __global__ __launch_bounds__(WG) void k_fused(FusedArgs A) {
     // largest CC; ties -> the component whose first edge comes first in the enumeration
     __syncthreads();
     uint64_t best = ~0ULL;
-    for (int i = tid; i < n; i += WG) {
+    for (int i = tid; i < n; i += FWG) {
       const int e0 = S.fwd[i], e1 = S.fwd[i + 1];
       if (e0 == e1) continue;
       const uint32_t r = S.parent[i];
@@ -430,19 +626,22 @@ __global__ __launch_bounds__(WG) void k_fused(FusedArgs A) {
       const int h = S.dst[e0];   // lists are sorted: the first target is the smallest key
       const int ph = picker_of<K>(c.pb, h);
       const uint64_t key = ((uint64_t)pair_index(pi, ph, K) << 48) |
-                           ((uint64_t)(i - c.pb[pi]) << 32) | ((uint64_t)(h - c.pb[ph]) << 16) | r;
+                           ((uint64_t)(i - picker_begin<K>(c.pb, pi)) << 32) |
+                           ((uint64_t)(h - picker_begin<K>(c.pb, ph)) << 16) | r;
       best = key < best ? key : best;
     }
-    best = block_min_u64(best, H.redu);
+    best = block_min_u64<FWG>(best, H.redu);
     if (tid == 0) H.target = (int)(best & 0xFFFF);
   }
   __syncthreads();
 
+  STOP_AFTER(3);
+  STAMP(8);
   // ---- P4: clique count per picker-0 root, vertex marking, output reservation
   c.set_order = 2 * K < H.nodes;
   const int n0 = c.pb[1];
   const int target = H.target;
-  for (int r = tid; r < n0; r += WG) {
+  for (int r = tid; r < n0; r += FWG) {
     uint32_t cntr = 0;
     if (S.fwd[r] < S.fwd[r + 1] && (!get_cc || S.parent[r] == (uint32_t)target)) {
       int mem[K];
@@ -454,7 +653,8 @@ __global__ __launch_bounds__(WG) void k_fused(FusedArgs A) {
     S.cnt[r] = cntr;
   }
   __syncthreads();
-  const int64_t C = block_scan_array(S.cnt, n0, H.red64);
+  STAMP(9);
+  const int64_t C = block_scan_array<FWG>(S.cnt, n0, H.red64);
   if (tid == 0) {
     S.cnt[n0] = (uint32_t)C;
     H.C = C;
@@ -468,40 +668,42 @@ __global__ __launch_bounds__(WG) void k_fused(FusedArgs A) {
   }
   __syncthreads();
 
+  STOP_AFTER(4);
+  STAMP(10);
   // ---- P5: row index = rank of each clique vertex by (x, y, id): x-major grid columns
   if (H.status == 0) {
     const int gx = H.gx, gy = H.gy;
     uint32_t* colc = S.parent;
-    for (int q = tid; q <= gx; q += WG) colc[q] = 0;
+    for (int q = tid; q <= gx; q += FWG) colc[q] = 0;
     __syncthreads();
-    for (int v = tid; v < n; v += WG) {
-      if (S.flags[v] != 3) continue;
-      int cx, cy;
-      cell_xm(H, S.xs[v], S.ys[v], &cx, &cy);
-      atomicAdd(&colc[cx], 1u);
-    }
+    for (int t = tid; t < n; t += FWG)
+      if (S.smark[t]) atomicAdd(&colc[S.scell[t] / gy], 1u);
     __syncthreads();
-    const int64_t V = block_scan_array(colc, gx, H.red64);
+    const int64_t V = block_scan_array<FWG>(colc, gx, H.red64);
     if (tid == 0) H.V = (int)V;
-    for (int v = tid; v < n; v += WG) {
-      if (S.flags[v] != 3) continue;
-      int cx, cy;
-      cell_xm(H, S.xs[v], S.ys[v], &cx, &cy);
-      const double xv = S.xs[v], yv = S.ys[v];
+    // rank inside the x-major grid column by (x, y, id); lanes walk sorted positions, so a
+    // wave shares its column (same trip count, broadcast reads)
+    for (int t = tid; t < n; t += FWG) {
+      if (!S.smark[t]) continue;
+      const int cx = S.scell[t] / gy;
+      const double2 v = S.sxy[t];
+      const int vi = S.citems[t];
       uint32_t rk = colc[cx];
       const int lo = S.cstart[cx * gy], hi = S.cstart[(cx + 1) * gy];
-      for (int t = lo; t < hi; ++t) {
-        const int u = S.citems[t];
-        if (S.flags[u] != 3) continue;
-        const double xu = S.xs[u], yu = S.ys[u];
-        rk += (xu < xv) || (xu == xv && (yu < yv || (yu == yv && u < v)));
+      for (int u = lo; u < hi; ++u) {
+        const uint8_t mk = S.smark[u];
+        const double2 w = S.sxy[u];
+        const int ui = S.citems[u];
+        rk += mk && ((w.x < v.x) || (w.x == v.x && (w.y < v.y || (w.y == v.y && ui < vi))));
       }
-      S.vrank[v] = (uint16_t)rk;
+      S.vrank[vi] = (uint16_t)rk;
     }
     __syncthreads();
 
+    STOP_AFTER(5);
+    STAMP(11);
     // ---- P6: clique fill + ILP epilogue + COO rows
-    for (int r = tid; r < n0; r += WG) {
+    for (int r = tid; r < n0; r += FWG) {
       if (S.cnt[r + 1] == S.cnt[r]) continue;
       int mem[K];
       mem[0] = r;
@@ -509,6 +711,7 @@ __global__ __launch_bounds__(WG) void k_fused(FusedArgs A) {
       FLevel<K, 1, true>::run(c, mem);
     }
   }
+  STAMP(12);
   if (tid == 0) {
     MgStat st = {};
     st.n_edges = H.E;
@@ -537,7 +740,7 @@ int launch_fused(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArg
         return -2;                                                                            \
       attr_set = true;                                                                        \
     }                                                                                         \
-    hipLaunchKernelGGL(k_fused<KK>, dim3(n_blocks), dim3(WG), lds_bytes, stream, A);          \
+    hipLaunchKernelGGL(k_fused<KK>, dim3(n_blocks), dim3(FWG), lds_bytes, stream, A);          \
     break;                                                                                    \
   }
     RGC_FUSED_CASE(2)

@@ -31,8 +31,8 @@ constexpr int RGC_ST_OVERFLOW = 4;   // output capacity exceeded: host grows and
 
 // LDS layout of the fused kernel for a size class (byte offsets into dynamic LDS)
 struct FusedLayout {
-  int off_xs, off_ys, off_cstart, off_cnt, off_fwd, off_parent, off_citems, off_vrank, off_flags,
-      off_dst, total;
+  int off_sxy, off_cstart, off_cnt, off_fwd, off_parent, off_citems, off_pos, off_scell, off_vrank,
+      off_flags, off_smark, off_dst, total;
 };
 
 struct FusedArgs {
@@ -54,6 +54,7 @@ struct FusedArgs {
   int32_t* consensus;
   int32_t* members;
   uint8_t* order;
+  unsigned long long* stamps;   // diagnostic build (RGC_STAMPS) only: 8 stamps per WG
 };
 
 int fused_lds_bytes(int nmax, int ecap);

@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librepic_gc.so")
+# REPIC_GC_LIB selects the diagnostic build (librepic_gc_diag.so) for tools/phase_stamps.py
+LIB_PATH = os.environ.get("REPIC_GC_LIB") or os.path.join(_HERE, "librepic_gc.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

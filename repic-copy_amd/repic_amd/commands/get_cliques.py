@@ -24,8 +24,7 @@ from .. import _lib
 from ..dist import exclusive_offsets, shard_bounds
 from ..ingest import DirIndex, list_methods, micrograph_names, plan, probe_start_method
 from ..pipeline import Batch, run_batch, split_batches
-from ..writers import (consensus_coords, constraint_matrix, multi_out_coords, write_micrograph,
-                       write_skip)
+from ..writers import Writer, consensus_coords, constraint_matrix, multi_out_coords
 
 name = "get_cliques"
 
@@ -64,7 +63,19 @@ def _dist_env():
 def main(args):
     """get_cliques.py:72-229 semantics; under torchrun (WORLD_SIZE > 1) every rank takes a
     contiguous shard of the micrographs on its own GPU."""
+    assert os.path.exists(args.in_dir), "Error - input directory does not exist"
     world, rank, local = _dist_env()
+    dev = args.device if getattr(args, "device", None) is not None else local
+    # the HIP context is created before torch.distributed is imported (a child that
+    # initialised gloo first could not see the device on the GPU pool)
+    ctx = _lib.Context(dev)
+    try:
+        _main(args, ctx, world, rank)
+    finally:
+        ctx.close()
+
+
+def _main(args, ctx, world, rank):
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -101,8 +112,6 @@ def main(args):
     results = {}
     t_dev = 0.0
     if ok:
-        dev = args.device if getattr(args, "device", None) is not None else local
-        ctx = _lib.Context(dev)
         counts = [sum(c.n for c in mg.coords) for mg in ok]
         for m0, m1 in split_batches(counts, getattr(args, "batch_boxes", 1 << 25)):
             part = ok[m0:m1]
@@ -114,7 +123,6 @@ def main(args):
             t_dev += time.time() - t0
             for j, mg in enumerate(part):
                 results[id(mg)] = (batch, j, res[j])
-        ctx.close()
     # first micrograph (global index) at which the reference would raise
     fail = None
     for i, mg in enumerate(mgs):
@@ -128,6 +136,16 @@ def main(args):
     else:
         gfail = fail
     share = (t_plan + t_dev) / max(1, len(mgs))
+    writer = Writer(getattr(args, "threads", None))
+    try:
+        _write_all(args, mgs, results, methods, k, lo, fail, gfail, share, writer)
+    finally:
+        writer.close()
+    sys.stdout.flush()
+
+
+def _write_all(args, mgs, results, methods, k, lo, fail, gfail, share, writer):
+    """Write outputs in reference order; raise the reference's exception where it would."""
     for i, mg in enumerate(mgs):
         if gfail is not None and lo + i > gfail:
             break
@@ -136,7 +154,7 @@ def main(args):
         print(f"\n--- {mg.base} ---\n")
         if mg.status == "skip":
             print("Skipping micrograph - not all methods have picked particles...")
-            write_skip(args.out_dir, mg.base)
+            writer.skip(args.out_dir, mg.base)
             continue
         if mg.status == "crash":
             raise mg.exc
@@ -164,6 +182,5 @@ def main(args):
             g = r.consensus.astype(np.int64)
             coords = consensus_coords(batch.x[g], batch.y[g], idb + g)
         A = constraint_matrix(r.rows, r.n_vert)
-        write_micrograph(args.out_dir, mg.base, r.w, coords, r.conf, A,
-                         share + (time.time() - t0), r.cc_max, r.cc_cnt)
-    sys.stdout.flush()
+        writer.micrograph(args.out_dir, mg.base, r.w, coords, r.conf, A,
+                          share + (time.time() - t0), r.cc_max, r.cc_cnt)

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import os
 import pickle
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 from scipy.sparse import coo_matrix
@@ -65,3 +66,46 @@ def write_micrograph(out_dir, base, w, coords, conf, A, seconds, cc_max, cc_cnt)
             pickle.dump(val, o, protocol=pickle.HIGHEST_PROTOCOL)
     with open(os.path.join(out_dir, f"{base}_runtime.tsv"), "wt") as o:
         o.write("\t".join([str(seconds), str(cc_max), str(cc_cnt)]) + "\n")
+
+
+class Writer:
+    """Thread-pooled writer: file creation dominates the per-micrograph output cost and
+    releases the GIL, so writes of different micrographs overlap.  ``close()`` waits for
+    every pending write and re-raises the first I/O error."""
+
+    def __init__(self, threads=None):
+        self.threads = threads or min(16, (os.cpu_count() or 1))
+        self._pool = ThreadPoolExecutor(max_workers=self.threads) if self.threads > 1 else None
+        self._futs = []
+        self._bases = set()
+
+    def _submit(self, fn, *args):
+        base = args[1]
+        if base in self._bases:      # same output name twice: keep the reference's order
+            self._drain()
+        self._bases.add(base)
+        if self._pool is None:
+            fn(*args)
+        else:
+            self._futs.append(self._pool.submit(fn, *args))
+            if len(self._futs) > 4 * self.threads:
+                self._drain(len(self._futs) // 2)
+
+    def _drain(self, n=None):
+        n = len(self._futs) if n is None else n
+        done, self._futs = self._futs[:n], self._futs[n:]
+        for f in done:
+            f.result()
+
+    def skip(self, out_dir, base):
+        self._submit(write_skip, out_dir, base)
+
+    def micrograph(self, *args):
+        self._submit(write_micrograph, *args)
+
+    def close(self):
+        try:
+            self._drain()
+        finally:
+            if self._pool is not None:
+                self._pool.shutdown(wait=True)

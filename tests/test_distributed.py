@@ -96,6 +96,7 @@ try:
     get_cliques.main(a)
 except Exception as e:
     exc = type(e).__name__
+    import traceback; traceback.print_exc()
 print(json.dumps({"exc": exc}))
 """
 
@@ -121,6 +122,8 @@ def test_cli_two_ranks_match_golden(name, tmp_path):
         o, e = p.communicate(timeout=600)
         assert p.returncode == 0, e[-3000:]
         excs.append(json.loads(o.strip().splitlines()[-1])["exc"])
+        if excs[-1] is not None and excs[-1] != meta["exception"]:
+            raise AssertionError(e[-3000:])
     if meta["exception"]:
         assert meta["exception"] in excs
     else:

@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Per-phase cycle shares of the fused kernel from the diagnostic build (RGC_STAMPS).
+
+  REPIC_GC_LIB=repic-copy_amd/repic_amd/librepic_gc_diag.so python tools/phase_stamps.py [C2] [n_mg]
+
+Prints, per phase, mean / p50 / p99 s_memtime cycles per workgroup, and the workgroup
+timeline (first start, last end) to see how many occupancy rounds the launch took.
+Shares only: the stamps add a barrier per phase (never quote this build's run time).
+"""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "repic-copy_amd"))
+os.environ.setdefault("REPIC_GC_LIB", os.path.join(ROOT, "repic-copy_amd/repic_amd/librepic_gc_diag.so"))
+
+import numpy as np  # noqa: E402
+
+from repic_amd import _lib, synth  # noqa: E402
+from repic_amd.pipeline import Batch  # noqa: E402
+
+cfg_name = sys.argv[1] if len(sys.argv) > 1 else "C2"
+n_mg = int(sys.argv[2]) if len(sys.argv) > 2 else 10000
+cfg = synth.SynthConfig(**synth.CONFIGS[cfg_name], seed=0)
+batch = Batch.pack(cfg.k, cfg.box, synth.batch(cfg, n_mg))
+ctx = _lib.Context(0)
+for _ in range(3):
+    r = ctx.run(batch.n_mg, cfg.k, cfg.box, batch.box_off, batch.id_base, batch.x, batch.y,
+                batch.score, 0)
+f = _lib.lib.rgc_diag_stamps
+f.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int64]
+f.restype = C.c_int64
+n = f(ctx._p, None, 0)
+buf = (C.c_uint64 * n)()
+f(ctx._p, buf, n)
+st = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 16).astype(np.int64)[:, :13]
+names = ["P0 load+bbox", "P1 grid+sort", "P2a stencil+scan", "P2b count walk", "P2c fwd scan",
+         "P2d fill walk", "P2e list sort", "P3 CC", "P4a DFS count", "P4b scan+reserve",
+         "P5 rank", "P6 fill+epilogue"]
+valid = (st != 0).all(axis=1)
+d = np.diff(st[valid], axis=1)
+tot = d.sum(axis=1)
+print(f"{cfg_name}: {n_mg} micrographs, {valid.sum()} complete WGs, cliques {r.n_cliques}")
+for i, nm in enumerate(names):
+    print(f"  {nm:18s} mean {d[:, i].mean():9.0f}  p50 {np.median(d[:, i]):9.0f}  "
+          f"p99 {np.percentile(d[:, i], 99):9.0f}  share {d[:, i].sum() / tot.sum():6.1%}")
+print(f"  per-WG total cycles: mean {tot.mean():.0f} p50 {np.median(tot):.0f} p99 {np.percentile(tot, 99):.0f}")
+span = st[valid, 12].max() - st[valid, 0].min()
+print(f"  launch span {span} cycles; sum(WG cycles)/span = {tot.sum() / span:.1f} concurrent WGs")
