@@ -116,6 +116,13 @@ void rgc_parsed_free(rgc_parsed* p);
 /* Host test hooks for the CPython set-order emulation (pyset.h). */
 uint64_t rgc_py_hash_node(double x, double y, int64_t id);
 int rgc_py_set_order(const uint64_t* hashes, int n, int8_t* out);
+/* Host test hook: the device ILP epilogue of ONE clique (rgc_device.h epilogue<K>), run on
+ * the CPU.  Members in picker order; ji[i*k+j] for i < j; ins only used when !set_order.
+ * Outputs: consensus member index, node-iteration order (k entries), w, conf.
+ * Reference: get_cliques.py:169-190 (median conf / w, weighted-degree consensus). */
+int rgc_test_epilogue(int k, const double* x, const double* y, const double* score,
+                      const int64_t* ids, const double* ji, int set_order, const uint64_t* ins,
+                      int* arg, int8_t* ord, float* w, float* conf);
 
 #ifdef __cplusplus
 }

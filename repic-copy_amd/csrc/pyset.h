@@ -132,4 +132,70 @@ PYS_FN int set_order(const uint64_t* hashes, int n, int8_t* out) {
   return r;
 }
 
+// ---- register-resident variant for the device epilogue (no stack arrays, so no scratch):
+// the 32-slot table lives in two u64 words as 4-bit slots (15 = empty), keys n <= 8 (a set of
+// <= 8 keys never grows past 32 slots: one resize at fill 5 -> 32).
+PYS_FN int pk_get(uint64_t lo, uint64_t hi, uint64_t i) {
+  return (int)(((i < 16 ? lo : hi) >> (4 * (i & 15))) & 15);
+}
+PYS_FN void pk_set(uint64_t& lo, uint64_t& hi, uint64_t i, int v) {
+  const uint64_t sh = 4 * (i & 15);
+  const uint64_t m = ~(15ULL << sh), b = (uint64_t)v << sh;
+  if (i < 16) lo = (lo & m) | b; else hi = (hi & m) | b;
+}
+PYS_FN uint64_t pk_probe(uint64_t lo, uint64_t hi, uint64_t mask, uint64_t hash) {
+  uint64_t perturb = hash;
+  uint64_t i = hash & mask;
+  while (true) {
+    if (pk_get(lo, hi, i) == 15) return i;
+    if (i + 9 <= mask) {
+      for (uint64_t j = 1; j <= 9; ++j)
+        if (pk_get(lo, hi, i + j) == 15) return i + j;
+    }
+    perturb >>= 5;
+    i = (i * 5 + 1 + perturb) & mask;
+  }
+}
+// Same result as set_order for N <= 8 keys, packed: nibble r = insertion index of the r-th
+// key yielded by iteration.  Every private array is indexed at compile time: the one resize a
+// set of <= 8 keys goes through (fill 5: 8 -> 32 slots) re-inserts the five keys in old-slot
+// order through a compare-exchange network instead of a table lookup.
+template <int N>
+PYS_FN uint32_t set_order_packed(const uint64_t (&h)[N]) {
+  static_assert(N >= 1 && N <= 8, "packed set order supports 1..8 keys");
+  uint64_t lo = ~0ULL, hi = ~0ULL, mask = 7;
+  uint64_t slot[N];
+#pragma unroll
+  for (int t = 0; t < N; ++t) {
+    slot[t] = pk_probe(lo, hi, mask, h[t]);
+    pk_set(lo, hi, slot[t], t);
+    if (t == 4) {   // fill 5: 5 * 5 >= 7 * 3 -> set_table_resize to 32 slots
+      uint64_t ks[5], kh[5];
+      int kt[5];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) { ks[i] = slot[i]; kh[i] = h[i]; kt[i] = i; }
+#pragma unroll
+      for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int q = 0; q < 4 - i; ++q)
+          if (ks[q] > ks[q + 1]) {
+            uint64_t tl = ks[q]; ks[q] = ks[q + 1]; ks[q + 1] = tl;
+            tl = kh[q]; kh[q] = kh[q + 1]; kh[q + 1] = tl;
+            const int ti = kt[q]; kt[q] = kt[q + 1]; kt[q + 1] = ti;
+          }
+      lo = ~0ULL; hi = ~0ULL;
+      mask = 31;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) pk_set(lo, hi, pk_probe(lo, hi, mask, kh[i]), kt[i]);
+    }
+  }
+  uint32_t out = 0;
+  int r = 0;
+  for (uint64_t i = 0; i <= mask; ++i) {
+    const int v = pk_get(lo, hi, i);
+    if (v != 15) { out |= (uint32_t)v << (4 * r); ++r; }
+  }
+  return out;
+}
+
 }  // namespace pyset

@@ -666,6 +666,22 @@ int64_t rgc_diag_stamps(rgc_ctx* c, uint64_t* out, int64_t max_n) {
 
 int rgc_py_set_order(const uint64_t* hashes, int n, int8_t* out) {
   if (n < 0 || n > 18) return fail("set_order supports 0..18 keys");
+  if (n >= 1 && n <= 8) {   // the register-packed variant the device epilogue uses
+    uint32_t p = 0;
+    switch (n) {
+#define RGC_SO(NN)                                  \
+  case NN: {                                        \
+    uint64_t h[NN];                                 \
+    for (int i = 0; i < NN; ++i) h[i] = hashes[i];  \
+    p = pyset::set_order_packed<NN>(h);             \
+    break;                                          \
+  }
+      RGC_SO(1) RGC_SO(2) RGC_SO(3) RGC_SO(4) RGC_SO(5) RGC_SO(6) RGC_SO(7) RGC_SO(8)
+#undef RGC_SO
+    }
+    for (int i = 0; i < n; ++i) out[i] = (int8_t)((p >> (4 * i)) & 15);
+    return n;
+  }
   return pyset::set_order(hashes, n, out);
 }
 

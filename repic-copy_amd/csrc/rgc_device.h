@@ -127,7 +127,7 @@ __device__ __forceinline__ int64_t block_scan_u16(uint16_t* a, int n, int64_t* l
 
 // ----------------------------------------------------------------------------- arithmetic
 // reference calc_jaccard (get_cliques.py:40-46), same f64 op order, no FMA.
-__device__ __forceinline__ double jaccard(double x, double y, double a, double b, double B,
+__host__ __device__ __forceinline__ double jaccard(double x, double y, double a, double b, double B,
                                           double two_b2) {
   const double xo = fmax((fmin(x, a) + B) - fmax(x, a), 0.0);
   const double yo = fmax((fmin(y, b) + B) - fmax(y, b), 0.0);
@@ -147,7 +147,7 @@ __device__ __forceinline__ bool is_edge(double xa, double ya, double xb, double 
 // two middle values ((a + b) / 2) for even n; NaN if any value is NaN.  Sorting network on a
 // register array (fully unrolled: no scratch).
 template <int N>
-__device__ __forceinline__ double median_n(double (&v)[N]) {
+__host__ __device__ __forceinline__ double median_n(double (&v)[N]) {
   bool nan = false;
 #pragma unroll
   for (int i = 0; i < N; ++i) nan |= isnan(v[i]);
@@ -180,11 +180,12 @@ struct Epi {
 // ji[i][j]: JI of members i < j;  s[i]: scores;  xs/ys: coordinates;  ids: global box ids
 // set_order: networkx iterates set(sorted(clique)) (2k < |G|) vs graph insertion order;
 // ins[i]  : graph insertion key of member i (used only when !set_order)
+// All private arrays are indexed with compile-time indices only (no scratch).
 template <int K>
-__device__ __forceinline__ void epilogue(const int (&mem)[K], const double (&ji)[K][K],
+__host__ __device__ __forceinline__ void epilogue(const int (&mem)[K], const double (&ji)[K][K],
                                          const double (&s)[K], const double (&xs)[K],
                                          const double (&ys)[K], const int64_t (&ids)[K],
-                                         bool set_order, const uint64_t* ins, bool need_order,
+                                         bool set_order, const uint64_t (&ins)[K], bool need_order,
                                          Epi<K>& out) {
   double sc[K];
 #pragma unroll
@@ -224,46 +225,68 @@ __device__ __forceinline__ void epilogue(const int (&mem)[K], const double (&ji)
     else if (deg[i] == dmax) ++nmax;
   }
   if (nmax > 1 || need_order) {
-    int8_t ord[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i) ord[i] = (int8_t)i;
+    // ord: nibble r = member index of the r-th node in networkx node-iteration order.
+    // Sorting is done by ranks (rank_i = number of members ordered before member i), so no
+    // private array is ever permuted or dynamically indexed.
+    uint32_t inv = 0;   // nibble t = member index at sorted position t
+    uint32_t ord = 0;
     if (set_order) {
       // insertion order = sorted (x, y, id); then CPython set iteration order
-      int8_t srt[K];
-#pragma unroll
-      for (int i = 0; i < K; ++i) srt[i] = (int8_t)i;
-      for (int i = 1; i < K; ++i) {
-        const int8_t t = srt[i];
-        int q = i - 1;
-        while (q >= 0) {
-          const int u = srt[q];
-          const bool gt = (xs[u] > xs[t]) ||
-                          (xs[u] == xs[t] && (ys[u] > ys[t] || (ys[u] == ys[t] && mem[u] > mem[t])));
-          if (!gt) break;
-          srt[q + 1] = srt[q];
-          --q;
-        }
-        srt[q + 1] = t;
-      }
       uint64_t hs[K];
-      for (int i = 0; i < K; ++i) hs[i] = pyset::hash_node(xs[srt[i]], ys[srt[i]], ids[srt[i]]);
-      int8_t so[K];
-      pyset::set_order(hs, K, so);
-      for (int i = 0; i < K; ++i) ord[i] = srt[so[i]];
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        int rk = 0;
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+          const bool lt = (xs[q] < xs[i]) ||
+                          (xs[q] == xs[i] && (ys[q] < ys[i] || (ys[q] == ys[i] && mem[q] < mem[i])));
+          rk += lt ? 1 : 0;
+        }
+        inv |= (uint32_t)i << (4 * rk);
+      }
+      // hashes in insertion (sorted) order: hs[t] = hash of the member at position t
+#pragma unroll
+      for (int t = 0; t < K; ++t) {
+        const int i = (inv >> (4 * t)) & 15;
+        double hx = xs[0], hy = ys[0];
+        int64_t hid = ids[0];
+#pragma unroll
+        for (int q = 1; q < K; ++q) {
+          const bool h = (i == q);
+          hx = h ? xs[q] : hx;
+          hy = h ? ys[q] : hy;
+          hid = h ? ids[q] : hid;
+        }
+        hs[t] = pyset::hash_node(hx, hy, hid);
+      }
+      const uint32_t so = pyset::set_order_packed<K>(hs);
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        const int t = (so >> (4 * r)) & 15;
+        ord |= ((inv >> (4 * t)) & 15) << (4 * r);
+      }
     } else {
-      for (int i = 1; i < K; ++i) {
-        const int8_t t = ord[i];
-        int q = i - 1;
-        while (q >= 0 && ins[ord[q]] > ins[t]) { ord[q + 1] = ord[q]; --q; }
-        ord[q + 1] = t;
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        int rk = 0;
+#pragma unroll
+        for (int q = 0; q < K; ++q) rk += (ins[q] < ins[i] || (ins[q] == ins[i] && q < i)) ? 1 : 0;
+        ord |= (uint32_t)i << (4 * rk);
       }
     }
     if (nmax > 1) {
-      for (int i = 0; i < K; ++i)
-        if (deg[ord[i]] == dmax) { arg = ord[i]; break; }
+      uint32_t top = 0;   // members whose degree equals the maximum
+#pragma unroll
+      for (int i = 0; i < K; ++i) top |= (deg[i] == dmax ? 1u : 0u) << i;
+      bool found = false;
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        const int mi = (ord >> (4 * r)) & 15;
+        if (!found && ((top >> mi) & 1u)) { arg = mi; found = true; }
+      }
     }
 #pragma unroll
-    for (int i = 0; i < K; ++i) out.ord[i] = ord[i];
+    for (int i = 0; i < K; ++i) out.ord[i] = (int8_t)((ord >> (4 * i)) & 15);
   }
   out.arg = arg;
 }

@@ -42,19 +42,23 @@ __host__ __device__ inline FusedLayout fused_layout(int nmax, int ecap) {
   FusedLayout L;
   auto al = [](int v) { return (v + 15) & ~15; };
   int o = al((int)sizeof(FusedHdr));
+  // live until the end of the kernel
   L.off_sxy = o; o += al(16 * nmax);          // (x, y) in cell-sorted order
-  L.off_cstart = o; o += al(2 * (4 * nmax + 8));   // u16 cell starts, <= 4n + 1 cells
   L.off_cnt = o; o += al(4 * (nmax + 4));
   L.off_fwd = o; o += al(4 * (nmax + 4));
+  L.off_pos = o; o += al(2 * nmax);           // local box index -> sorted position
+  L.off_vrank = o; o += al(2 * nmax);
+  L.off_dst = o; o += al(2 * ecap);
+  // dead after P5: reused in P6 as f64 scores (8 n) + the clique member buffer
+  L.off_union = o;
+  L.off_cstart = o; o += al(2 * (4 * nmax + 8));   // u16 cell starts, <= 4n + 1 cells
   L.off_parent = o; o += al(4 * (nmax + 4));
   L.off_citems = o; o += al(2 * nmax);        // sorted position -> local box index
-  L.off_pos = o; o += al(2 * nmax);           // local box index -> sorted position
   L.off_scell = o; o += al(2 * nmax);         // sorted position -> cell
-  L.off_vrank = o; o += al(2 * nmax);
   L.off_flags = o; o += al(nmax);             // by local index
   L.off_smark = o; o += al(nmax);             // clique-vertex mark by sorted position
-  L.off_dst = o; o += al(2 * ecap);
   L.total = o;
+  L.off_cbuf = L.off_union + al(8 * nmax);
   return L;
 }
 
@@ -73,6 +77,8 @@ struct FShared {
   uint8_t* flags;   // by local index: 0 no edge, 1 graph node, 3 clique vertex
   uint8_t* smark;   // by sorted position: 1 clique vertex
   uint16_t* dst;
+  double* sscore;   // P6 only (union region): scores of clique vertices by local index
+  uint16_t* cbuf;   // P6 only (union region): members of the current clique chunk
 };
 
 template <int K>
@@ -93,7 +99,8 @@ struct FCtx {
   int m, b0, n;
   int64_t idb;       // global id of local box 0
   bool set_order;    // networkx iterates set(sorted(clique)) (2k < |G|)
-  int64_t out;       // next output clique index (fill)
+  int64_t out;       // next clique index within the micrograph (fill)
+  int64_t c0, c1;    // clique chunk being buffered in cbuf (fill)
   int64_t count;
 };
 
@@ -120,19 +127,21 @@ __device__ __forceinline__ int picker_of(const int (&pb)[K + 1], int i) {
   for (int q = 1; q < K; ++q) p += (i >= pb[q]);
   return p;
 }
-// first box index after box i's picker (unrolled select, no dynamic indexing)
+// first box index after box i's picker.  Written as sums of differences, never as a select
+// between array elements: the optimiser folds such selects into a dynamically indexed load,
+// which would move the whole context struct to scratch.
 template <int K>
 __device__ __forceinline__ int picker_end(const int (&pb)[K + 1], int i) {
-  int e = pb[K];
+  int e = pb[1];
 #pragma unroll
-  for (int q = K - 1; q >= 1; --q) e = (i < pb[q]) ? pb[q] : e;
+  for (int q = 1; q < K; ++q) e += (i >= pb[q]) ? (pb[q + 1] - pb[q]) : 0;
   return e;
 }
 template <int K>
 __device__ __forceinline__ int picker_begin(const int (&pb)[K + 1], int p) {
   int b = pb[0];
 #pragma unroll
-  for (int q = 1; q < K; ++q) b = (p == q) ? pb[q] : b;
+  for (int q = 1; q < K; ++q) b += (p >= q) ? (pb[q] - pb[q - 1]) : 0;
   return b;
 }
 
@@ -159,7 +168,7 @@ __device__ __forceinline__ int cell_xm(const FusedHdr& H, double x, double y, in
 // graph insertion key of a clique vertex (tiny graphs only): first appearance of the node in
 // the edge enumeration (picker pair, a index, b index, side), get_cliques.py:33-34,135-143
 template <int K>
-__device__ uint64_t ins_key(const FCtx<K>& c, int u) {
+__device__ __forceinline__ uint64_t ins_key(const FCtx<K>& c, int u) {
   const int pu = picker_of<K>(c.pb, u);
   const int bu = picker_begin<K>(c.pb, pu);
   const int lu = u - bu;
@@ -176,18 +185,19 @@ __device__ uint64_t ins_key(const FCtx<K>& c, int u) {
          ((uint64_t)(d0 - picker_begin<K>(c.pb, pd)) << 1);
 }
 
+// ILP epilogue of one buffered clique (thread per clique): reference get_cliques.py:169-202.
+// j = output index; mem = local box indices in picker order.  Scores come from LDS.
 template <int K>
-__device__ void fused_emit(FCtx<K>& c, const int (&mem)[K]) {
-  const int64_t j = c.out++;
+__device__ __forceinline__ void fused_epilogue(const FCtx<K>& c, int64_t j, const int (&mem)[K]) {
   double ji[K][K], s[K], xs[K], ys[K];
   int64_t ids[K];
-  uint64_t ins[K];
+  uint64_t ins[K] = {};
 #pragma unroll
   for (int i = 0; i < K; ++i) {
     const double2 xy = c.S.sxy[c.S.pos[mem[i]]];
     xs[i] = xy.x;
     ys[i] = xy.y;
-    s[i] = c.score[c.b0 + mem[i]];
+    s[i] = c.S.sscore[mem[i]];
     ids[i] = c.idb + mem[i];
   }
 #pragma unroll
@@ -233,7 +243,7 @@ __device__ void fused_emit(FCtx<K>& c, const int (&mem)[K]) {
 // the picker-(D-1) member that are also forward neighbours of every earlier member.
 template <int K, int D, bool FILL>
 struct FLevel {
-  __device__ static void run(FCtx<K>& c, int (&mem)[K]) {
+  __device__ __forceinline__ static void run(FCtx<K>& c, int (&mem)[K]) {
     const int prev = mem[D - 1];
     const int l0 = c.S.fwd[prev], h0 = c.S.fwd[prev + 1];
     const int lo = lb16(c.S.dst, l0, h0, c.pb[D]);
@@ -253,9 +263,14 @@ struct FLevel {
 };
 template <int K, bool FILL>
 struct FLevel<K, K, FILL> {
-  __device__ static void run(FCtx<K>& c, int (&mem)[K]) {
+  __device__ __forceinline__ static void run(FCtx<K>& c, int (&mem)[K]) {
     if (FILL) {
-      fused_emit<K>(c, mem);
+      const int64_t j = c.out++;
+      if (j >= c.c0 && j < c.c1) {
+        uint16_t* dstb = c.S.cbuf + (j - c.c0) * K;
+#pragma unroll
+        for (int i = 0; i < K; ++i) dstb[i] = (uint16_t)mem[i];
+      }
     } else {
       ++c.count;
 #pragma unroll
@@ -371,6 +386,9 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
   S.flags = reinterpret_cast<uint8_t*>(smem + L.off_flags);
   S.smark = reinterpret_cast<uint8_t*>(smem + L.off_smark);
   S.dst = reinterpret_cast<uint16_t*>(smem + L.off_dst);
+  S.sscore = reinterpret_cast<double*>(smem + L.off_union);
+  S.cbuf = reinterpret_cast<uint16_t*>(smem + L.off_cbuf);
+  const int cbuf_cap = (L.total - L.off_cbuf) / (2 * K);   // cliques per P6 chunk
   const int tid = threadIdx.x;
   const int m = A.mg_list[blockIdx.x];
 #ifdef RGC_STAMPS
@@ -702,13 +720,34 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
 
     STOP_AFTER(5);
     STAMP(11);
-    // ---- P6: clique fill + ILP epilogue + COO rows
-    for (int r = tid; r < n0; r += FWG) {
-      if (S.cnt[r + 1] == S.cnt[r]) continue;
-      int mem[K];
-      mem[0] = r;
-      c.out = H.base + S.cnt[r];
-      FLevel<K, 1, true>::run(c, mem);
+    // ---- P6: stage the clique vertices' scores in LDS (the union region is dead now), then
+    // per chunk of <= cbuf_cap cliques: DFS fill of the member buffer (thread per root), then
+    // the ILP epilogue + COO rows with one thread per clique (coalesced output stores).
+    for (int i = tid; i < n; i += FWG)
+      if (S.flags[i] == 3) S.sscore[i] = c.score[b0 + i];
+    __syncthreads();
+    const int64_t Cm = H.C;
+    for (int64_t c0 = 0; c0 < Cm; c0 += cbuf_cap) {
+      const int64_t c1 = min(Cm, c0 + (int64_t)cbuf_cap);
+      c.c0 = c0;
+      c.c1 = c1;
+      for (int r = tid; r < n0; r += FWG) {
+        const int64_t lo = S.cnt[r], hi = S.cnt[r + 1];
+        if (lo == hi || hi <= c0 || lo >= c1) continue;
+        int mem[K];
+        mem[0] = r;
+        c.out = lo;
+        FLevel<K, 1, true>::run(c, mem);
+      }
+      __syncthreads();
+      for (int64_t j = c0 + tid; j < c1; j += FWG) {
+        int mem[K];
+        const uint16_t* sb = S.cbuf + (j - c0) * K;
+#pragma unroll
+        for (int i = 0; i < K; ++i) mem[i] = sb[i];
+        fused_epilogue<K>(c, H.base + j, mem);
+      }
+      __syncthreads();
     }
   }
   STAMP(12);

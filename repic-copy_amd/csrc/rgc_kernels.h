@@ -31,8 +31,8 @@ constexpr int RGC_ST_OVERFLOW = 4;   // output capacity exceeded: host grows and
 
 // LDS layout of the fused kernel for a size class (byte offsets into dynamic LDS)
 struct FusedLayout {
-  int off_sxy, off_cstart, off_cnt, off_fwd, off_parent, off_citems, off_pos, off_scell, off_vrank,
-      off_flags, off_smark, off_dst, total;
+  int off_sxy, off_cnt, off_fwd, off_pos, off_vrank, off_dst, off_union, off_cstart, off_parent,
+      off_citems, off_scell, off_flags, off_smark, off_cbuf, total;
 };
 
 struct FusedArgs {

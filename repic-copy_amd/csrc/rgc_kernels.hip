@@ -469,7 +469,7 @@ __device__ void emit_clique(const CliqueArgs& A, Walk<K>& W) {
   const int m = W.m;
   double s[K], xs[K], ys[K];
   int64_t ids[K];
-  uint64_t ins[K];
+  uint64_t ins[K] = {};
   const int64_t idb = A.id_base[m] - (int64_t)A.box_off[m * A.k];
 #pragma unroll
   for (int i = 0; i < K; ++i) {
@@ -489,7 +489,10 @@ __device__ void emit_clique(const CliqueArgs& A, Walk<K>& W) {
   epilogue<K>(W.mem, W.ji, s, xs, ys, ids, set_order, ins, multi, e);
   A.w[j] = e.w;
   A.conf[j] = e.conf;
-  A.consensus[j] = W.mem[e.arg];
+  int cons = W.mem[0];
+#pragma unroll
+  for (int i = 1; i < K; ++i) cons = (e.arg == i) ? W.mem[i] : cons;
+  A.consensus[j] = cons;
 #pragma unroll
   for (int i = 0; i < K; ++i) {
     A.members[j * K + i] = W.mem[i];
@@ -826,3 +829,43 @@ void launch_mg_offsets(hipStream_t stream, int n_mg, int k, const int32_t* box_o
 }
 
 }  // namespace rgc
+
+namespace {
+template <int K>
+int test_epilogue_k(const double* x, const double* y, const double* score, const int64_t* ids,
+                    const double* ji, int set_order, const uint64_t* ins, int* arg, int8_t* ord,
+                    float* w, float* conf) {
+  int mem[K];
+  double jj[K][K] = {}, s[K], xs[K], ys[K];
+  int64_t id[K];
+  uint64_t in[K];
+  int64_t idmin = ids[0];
+  for (int i = 1; i < K; ++i) idmin = ids[i] < idmin ? ids[i] : idmin;
+  for (int i = 0; i < K; ++i) {
+    mem[i] = (int)(ids[i] - idmin);   // any handle monotone in id
+    s[i] = score[i]; xs[i] = x[i]; ys[i] = y[i]; id[i] = ids[i];
+    in[i] = ins ? ins[i] : 0;
+    for (int j = i + 1; j < K; ++j) jj[i][j] = ji[i * K + j];
+  }
+  rgc::Epi<K> e;
+  rgc::epilogue<K>(mem, jj, s, xs, ys, id, set_order != 0, in, true, e);
+  *arg = e.arg;
+  for (int i = 0; i < K; ++i) ord[i] = e.ord[i];
+  *w = e.w;
+  *conf = e.conf;
+  return 0;
+}
+}  // namespace
+
+extern "C" int rgc_test_epilogue(int k, const double* x, const double* y, const double* score,
+                                 const int64_t* ids, const double* ji, int set_order,
+                                 const uint64_t* ins, int* arg, int8_t* ord, float* w,
+                                 float* conf) {
+  switch (k) {
+#define RGC_TE(KK) \
+  case KK: return test_epilogue_k<KK>(x, y, score, ids, ji, set_order, ins, arg, ord, w, conf);
+    RGC_TE(2) RGC_TE(3) RGC_TE(4) RGC_TE(5) RGC_TE(6) RGC_TE(7) RGC_TE(8)
+#undef RGC_TE
+    default: return -1;
+  }
+}

@@ -70,10 +70,13 @@ lib.rgc_parsed_free.restype = None
 lib.rgc_py_hash_node.argtypes = [C.c_double, C.c_double, C.c_int64]
 lib.rgc_py_hash_node.restype = C.c_uint64
 lib.rgc_py_set_order.argtypes = [C.POINTER(C.c_uint64), C.c_int, C.POINTER(C.c_int8)]
+lib.rgc_test_epilogue.argtypes = [C.c_int, _f64p, _f64p, _f64p, C.POINTER(C.c_int64), _f64p,
+                                  C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_int),
+                                  C.POINTER(C.c_int8), _f32p, _f32p]
 
 EXPORTS = ["rgc_abi_version", "rgc_last_error", "rgc_device_count", "rgc_ctx_create",
            "rgc_ctx_destroy", "rgc_run", "rgc_kernel_times", "rgc_parse_files",
-           "rgc_parsed_free", "rgc_py_hash_node", "rgc_py_set_order"]
+           "rgc_parsed_free", "rgc_py_hash_node", "rgc_py_set_order", "rgc_test_epilogue"]
 
 
 class RGCError(RuntimeError):
@@ -128,6 +131,25 @@ def py_set_order(hashes):
     o = (C.c_int8 * max(n, 1))()
     _check(lib.rgc_py_set_order(h, n, o))
     return [o[i] for i in range(n)]
+
+
+def test_epilogue(x, y, score, ids, ji, set_order=True, ins=None):
+    """The device ILP epilogue of one clique, run on the host (test hook):
+    -> (consensus member index, node-iteration order, w, conf)."""
+    k = len(x)
+    f = lambda a: np.ascontiguousarray(a, dtype=np.float64)  # noqa: E731
+    xa, ya, sa, ja = f(x), f(y), f(score), f(np.asarray(ji).reshape(k * k))
+    ia = np.ascontiguousarray(ids, dtype=np.int64)
+    insa = None if ins is None else (C.c_uint64 * k)(*[int(v) for v in ins])
+    arg = C.c_int(0)
+    ordr = (C.c_int8 * k)()
+    w, conf = C.c_float(0), C.c_float(0)
+    p64 = lambda a: a.ctypes.data_as(_f64p)  # noqa: E731
+    _check(lib.rgc_test_epilogue(k, p64(xa), p64(ya), p64(sa),
+                                 ia.ctypes.data_as(C.POINTER(C.c_int64)), p64(ja),
+                                 int(set_order), insa, C.byref(arg), ordr, C.byref(w),
+                                 C.byref(conf)))
+    return arg.value, [ordr[i] for i in range(k)], np.float32(w.value), np.float32(conf.value)
 
 
 # ----------------------------------------------------------------------------- device context
