@@ -33,6 +33,7 @@ struct FusedHdr {
   uint64_t redu[FNW];
   int redi[FNW];
   double minx, miny, cell;
+  float inv_gy;
   int gx, gy, ncell;
   int E, nodes, cc_cnt, cc_max, target, V, status;
   int64_t C, base;
@@ -299,7 +300,11 @@ __device__ __forceinline__ void stencil_setup(Stencil& st, int ts, const FShared
   st.L0 = st.L01 = st.L = 0;
   if (q >= H.ncell) return;
   const int gy = H.gy;
-  const int cx = q / gy, cy = q - cx * gy;
+  // q / gy through a float reciprocal, corrected to the exact quotient (q < 2^16)
+  int cx = (int)((float)q * H.inv_gy);
+  cx += ((cx + 1) * gy <= q) ? 1 : 0;
+  cx -= (cx * gy > q) ? 1 : 0;
+  const int cy = q - cx * gy;
   const int y0 = max(cy - 1, 0), y1 = min(cy + 1, gy - 1);
   int l0 = 0, h0 = 0, l1, h1, l2 = 0, h2 = 0;
   if (cx > 0) { l0 = S.cstart[(cx - 1) * gy + y0]; h0 = S.cstart[(cx - 1) * gy + y1 + 1]; }
@@ -327,44 +332,66 @@ __device__ __forceinline__ bool edge_test(double2 a, double2 b, double B, double
   return inter / (two_b2 - inter) > 0.3;                      // reference quotient
 }
 
-// Walk work items [w0, w1) (a contiguous chunk of the flattened (box, candidate) list).
-// FILL = 0: JI test, set the item's bit, count the edge for the owning box.
-// FILL = 1: replay the bits (or re-test when the bitmap did not fit) and append targets.
-template <int K, int FILL>
-__device__ __forceinline__ void walk_items(const FShared& S, const FusedHdr& H,
-                                           const int (&pb)[K + 1], const uint32_t* woff, int n,
-                                           int w0, int w1, uint32_t* ebits, bool use_bits,
-                                           double B, double two_b2, double i_lo, double i_hi) {
-  if (w0 >= w1) return;
-  int lo = 0, hi = n;                     // last ts with woff[ts] <= w0
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if ((int)woff[mid] <= w0) lo = mid; else hi = mid - 1;
-  }
-  int ts = lo;
-  Stencil st;
-  stencil_setup<K>(st, ts, S, H, pb);
-  int kk = w0 - (int)woff[ts];
-  for (int w = w0; w < w1; ++w, ++kk) {
-    while (kk >= st.L) {
-      ++ts;
-      kk = 0;
-      stencil_setup<K>(st, ts, S, H, pb);
-    }
-    const int t = kk < st.L0 ? st.lo0 + kk
-                             : (kk < st.L01 ? st.lo1 + (kk - st.L0) : st.lo2 + (kk - st.L01));
-    const int j = S.citems[t];
-    if (j < st.pe) continue;
-    if (FILL == 0) {
+// sorted position of stencil candidate kk (kk < st.L)
+__device__ __forceinline__ int stencil_pos(const Stencil& st, int kk) {
+  return kk < st.L0 ? st.lo0 + kk : (kk < st.L01 ? st.lo1 + (kk - st.L0) : st.lo2 + (kk - st.L01));
+}
+
+// P2 count for the box at sorted position ts (thread per box): JI test against every stencil
+// candidate of a higher picker; returns the edge count and the bitmask of edge candidates
+// (candidates 0..31; boxes with more candidates are re-tested by the fill).
+template <int K>
+__device__ __forceinline__ int pairs_count(const Stencil& st, const FShared& S, double B,
+                                           double two_b2, double i_lo, double i_hi,
+                                           uint32_t* mask_out) {
+  uint32_t mask = 0;
+  int cnt = 0;
+  int kk = 0;
+  const int los[3] = {st.lo0, st.lo1, st.lo2};
+  const int lens[3] = {st.L0, st.L01 - st.L0, st.L - st.L01};
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const int lo = los[r], hi = los[r] + lens[r];
+    for (int t = lo; t < hi; ++t, ++kk) {
+      const int j = S.citems[t];
+      if (j < st.pe) continue;
       if (edge_test(st.a, S.sxy[t], B, two_b2, i_lo, i_hi)) {
-        if (use_bits) atomicOr(&ebits[w >> 5], 1u << (w & 31));
-        atomicAdd(&S.fwd[st.i], 1u);
+        ++cnt;
+        mask |= (kk < 32) ? (1u << kk) : 0u;
       }
-    } else {
-      const bool e = use_bits ? ((ebits[w >> 5] >> (w & 31)) & 1u)
-                              : edge_test(st.a, S.sxy[t], B, two_b2, i_lo, i_hi);
-      if (e) S.dst[atomicAdd(&S.cnt[st.i], 1u)] = (uint16_t)j;
     }
+  }
+  *mask_out = mask;
+  return cnt;
+}
+
+// P2 fill: write the box's forward targets at dst[base..) from the count's bitmask (or by
+// re-testing), then sort them by target (insertion sort; lists are short).
+template <int K>
+__device__ __forceinline__ void pairs_fill(const Stencil& st, const FShared& S, uint32_t mask,
+                                           int base, int cnt, double B, double two_b2,
+                                           double i_lo, double i_hi) {
+  uint16_t* d = S.dst + base;
+  int c = 0;
+  if (st.L <= 32) {
+    while (mask) {
+      const int kk = __builtin_ctz(mask);
+      mask &= mask - 1;
+      d[c++] = S.citems[stencil_pos(st, kk)];
+    }
+  } else {
+    for (int kk = 0; kk < st.L; ++kk) {
+      const int t = stencil_pos(st, kk);
+      const int j = S.citems[t];
+      if (j < st.pe) continue;
+      if (edge_test(st.a, S.sxy[t], B, two_b2, i_lo, i_hi)) d[c++] = (uint16_t)j;
+    }
+  }
+  for (int a = 1; a < cnt; ++a) {
+    const uint16_t key = d[a];
+    int b = a - 1;
+    while (b >= 0 && d[b] > key) { d[b + 1] = d[b]; --b; }
+    d[b + 1] = key;
   }
 }
 
@@ -471,6 +498,7 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
       }
       H.ncell = H.gx * H.gy;
     }
+    H.inv_gy = H.gy > 0 ? 1.0f / (float)H.gy : 0.0f;
   }
   __syncthreads();
   const int nc = H.ncell;
@@ -511,10 +539,8 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
 
   STOP_AFTER(1);
   STAMP(2);
-  // ---- P2: Jaccard pairs (forward edges to higher pickers).
-  // Work items = (box, stencil candidate).  Per-box item counts are scanned and every lane
-  // takes an equal contiguous chunk of items, so no lane waits on a long candidate list of
-  // its neighbour.  The count pass records one bit per item; the fill pass replays the bits.
+  // ---- P2: Jaccard pairs (forward edges to higher pickers): count (JI test, edge bitmask
+  // per box) -> scan -> fill (bitmask replay, no atomics) + per-list sort.
   const double B = A.B, two_b2 = A.two_b2;
   // JI > 0.3  <=>  I > (6/13) B^2 exactly; decide without the division unless I lies within a
   // 2^-40 relative band of the threshold, where the reference's f64 quotient is evaluated.
@@ -522,27 +548,18 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
   // band moves the quotient by >= 1.1e-12 relative), so the decision is the reference's.
   const double t_star = 0.6 * B * B / 1.3;
   const double i_lo = t_star * (1.0 - 0x1p-40), i_hi = t_star * (1.0 + 0x1p-40);
-  uint32_t* woff = S.parent;                                   // dead until P3
-  uint32_t* ebits = reinterpret_cast<uint32_t*>(S.vrank);     // dead until P5: 16 bits / box
+  // thread per box (sorted position): lanes of a wave hold neighbouring boxes, so their
+  // stencils overlap (similar trip counts, broadcast LDS reads).  cnt[] (dead until P3) keeps
+  // each box's edge bitmask for the fill.
   for (int ts = tid; ts < n; ts += FWG) {
     Stencil st;
     stencil_setup<K>(st, ts, S, H, c.pb);
-    woff[ts] = st.L;
+    uint32_t mask;
+    S.fwd[st.i] = (uint32_t)pairs_count<K>(st, S, B, two_b2, i_lo, i_hi, &mask);
+    S.cnt[ts] = mask;
   }
-  for (int i = tid; i < n; i += FWG) S.fwd[i] = 0;
   __syncthreads();
-  const int W = (int)block_scan_array<FWG>(woff, n, H.red64);
   STAMP(3);
-  if (tid == 0) woff[n] = W;
-  const bool use_bits = W <= 16 * n - 64;   // bitmap fits the vrank region
-  if (use_bits)
-    for (int q = tid; q < (W + 31) / 32; q += FWG) ebits[q] = 0;
-  __syncthreads();
-  const int chunk = (W + FWG - 1) / FWG;
-  const int w0 = min(W, tid * chunk), w1 = min(W, w0 + chunk);
-  // count pass
-  walk_items<K, 0>(S, H, c.pb, woff, n, w0, w1, ebits, use_bits, B, two_b2, i_lo, i_hi);
-  __syncthreads();
   STAMP(4);
   const int64_t E = block_scan_array<FWG>(S.fwd, n, H.red64);
   if (tid == 0) {
@@ -551,24 +568,17 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
     if (E == 0) H.status = RGC_ST_NO_EDGES;
     else if (E > A.ecap) H.status = RGC_ST_DEFER;
   }
-  for (int i = tid; i < n; i += FWG) S.cnt[i] = S.fwd[i];
   __syncthreads();
   STAMP(5);
   if (H.status == 0) {
-    // fill pass, then sort every forward list by target (picker-major = id order)
-    walk_items<K, 1>(S, H, c.pb, woff, n, w0, w1, ebits, use_bits, B, two_b2, i_lo, i_hi);
-    __syncthreads();
-    STAMP(6);
-    for (int i = tid; i < n; i += FWG) {
-      const int base = S.fwd[i], end = S.fwd[i + 1];
-      for (int a = base + 1; a < end; ++a) {
-        const uint16_t key = S.dst[a];
-        int b = a - 1;
-        while (b >= base && S.dst[b] > key) { S.dst[b + 1] = S.dst[b]; --b; }
-        S.dst[b + 1] = key;
-      }
+    for (int ts = tid; ts < n; ts += FWG) {
+      Stencil st;
+      stencil_setup<K>(st, ts, S, H, c.pb);
+      const int base = S.fwd[st.i];
+      pairs_fill<K>(st, S, S.cnt[ts], base, (int)S.fwd[st.i + 1] - base, B, two_b2, i_lo, i_hi);
     }
     __syncthreads();
+    STAMP(6);
   }
   if (H.status != 0) {
     if (tid == 0) {
