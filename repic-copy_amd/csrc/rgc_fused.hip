@@ -33,9 +33,11 @@ struct FusedHdr {
   uint64_t redu[FNW];
   int redi[FNW];
   double minx, miny, cell;
+  double xbs;       // P5 x-bucket scale: bucket(x) = min(trunc((x - minx) * xbs), n - 1)
   float inv_gy;
   int gx, gy, ncell;
   int E, nodes, cc_cnt, cc_max, target, V, status;
+  uint32_t ccur;    // P4 clique-queue cursor
   int64_t C, base;
 };
 
@@ -50,7 +52,8 @@ __host__ __device__ inline FusedLayout fused_layout(int nmax, int ecap) {
   L.off_pos = o; o += al(2 * nmax);           // local box index -> sorted position
   L.off_vrank = o; o += al(2 * nmax);
   L.off_dst = o; o += al(2 * ecap);
-  // dead after P5: reused in P6 as f64 scores (8 n) + the clique member buffer
+  // P1-P3 grid and union-find; the cell starts (dead after P2) become the clique buffer of
+  // P4-P6, parent..scell (dead after P5) the f64 scores of P6
   L.off_union = o;
   L.off_cstart = o; o += al(2 * (4 * nmax + 8));   // u16 cell starts, <= 4n + 1 cells
   L.off_parent = o; o += al(4 * (nmax + 4));
@@ -59,7 +62,7 @@ __host__ __device__ inline FusedLayout fused_layout(int nmax, int ecap) {
   L.off_flags = o; o += al(nmax);             // by local index
   L.off_smark = o; o += al(nmax);             // clique-vertex mark by sorted position
   L.total = o;
-  L.off_cbuf = L.off_union + al(8 * nmax);
+  L.off_cbuf = L.off_cstart;
   return L;
 }
 
@@ -78,8 +81,8 @@ struct FShared {
   uint8_t* flags;   // by local index: 0 no edge, 1 graph node, 3 clique vertex
   uint8_t* smark;   // by sorted position: 1 clique vertex
   uint16_t* dst;
-  double* sscore;   // P6 only (union region): scores of clique vertices by local index
-  uint16_t* cbuf;   // P6 only (union region): members of the current clique chunk
+  double* sscore;   // P6 only (parent..scell): scores of clique vertices by local index
+  uint16_t* cbuf;   // P4-P6 (cell starts): clique queue, or the current chunk of the re-walk
 };
 
 template <int K>
@@ -103,6 +106,9 @@ struct FCtx {
   int64_t out;       // next clique index within the micrograph (fill)
   int64_t c0, c1;    // clique chunk being buffered in cbuf (fill)
   int64_t count;
+  uint16_t* cq_ord;  // P4 queue: ordinal of each queued clique within its root's DFS
+  uint32_t* ccur;    // P4 queue cursor (LDS)
+  int cq_cap;        // P4 queue capacity (cliques)
 };
 
 __device__ __forceinline__ uint32_t lds_ld(uint32_t* p) {
@@ -273,7 +279,15 @@ struct FLevel<K, K, FILL> {
         for (int i = 0; i < K; ++i) dstb[i] = (uint16_t)mem[i];
       }
     } else {
-      ++c.count;
+      // queue the clique (members + ordinal within the root's DFS) while the queue has room;
+      // its output index is known once the per-root counts are scanned
+      const uint32_t o = (uint32_t)c.count++;
+      const uint32_t slot = atomicAdd(c.ccur, 1u);
+      if (slot < (uint32_t)c.cq_cap) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) c.S.cbuf[slot * K + i] = (uint16_t)mem[i];
+        c.cq_ord[slot] = (uint16_t)o;
+      }
 #pragma unroll
       for (int i = 0; i < K; ++i) {
         c.S.flags[mem[i]] = 3;
@@ -413,9 +427,10 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
   S.flags = reinterpret_cast<uint8_t*>(smem + L.off_flags);
   S.smark = reinterpret_cast<uint8_t*>(smem + L.off_smark);
   S.dst = reinterpret_cast<uint16_t*>(smem + L.off_dst);
-  S.sscore = reinterpret_cast<double*>(smem + L.off_union);
+  S.sscore = reinterpret_cast<double*>(smem + L.off_parent);
   S.cbuf = reinterpret_cast<uint16_t*>(smem + L.off_cbuf);
-  const int cbuf_cap = (L.total - L.off_cbuf) / (2 * K);   // cliques per P6 chunk
+  const int cbuf_bytes = L.off_parent - L.off_cbuf;
+  const int cbuf_cap = cbuf_bytes / (2 * K);         // cliques per P6 re-walk chunk
   const int tid = threadIdx.x;
   const int m = A.mg_list[blockIdx.x];
 #ifdef RGC_STAMPS
@@ -479,7 +494,7 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
   // edge inside the 3x3 stencil while the stencil area is 3.4x smaller than with side B.
   if (tid == 0) {
     H.minx = mnx; H.miny = mny; H.cell = A.B; H.gx = 0; H.gy = 0; H.ncell = 0;
-    H.status = 0; H.C = 0; H.base = 0; H.V = 0; H.target = -1;
+    H.status = 0; H.C = 0; H.base = 0; H.V = 0; H.target = -1; H.ccur = 0;
     if (mnx <= mxx && A.B > 0.0) {
       const double ex = mxx - mnx, ey = mxy - mny;
       if (!(ex < 0x1p40 && ey < 0x1p40)) {
@@ -499,6 +514,8 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
       H.ncell = H.gx * H.gy;
     }
     H.inv_gy = H.gy > 0 ? 1.0f / (float)H.gy : 0.0f;
+    const double ex = mxx - mnx;
+    H.xbs = (mnx < mxx && ex < 0x1p60) ? (double)n / ex : 0.0;
   }
   __syncthreads();
   const int nc = H.ncell;
@@ -667,6 +684,9 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
   STAMP(8);
   // ---- P4: clique count per picker-0 root, vertex marking, output reservation
   c.set_order = 2 * K < H.nodes;
+  c.cq_cap = cbuf_bytes / (2 * K + 2);
+  c.cq_ord = S.cbuf + c.cq_cap * K;
+  c.ccur = &H.ccur;
   const int n0 = c.pb[1];
   const int target = H.target;
   for (int r = tid; r < n0; r += FWG) {
@@ -698,31 +718,41 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
 
   STOP_AFTER(4);
   STAMP(10);
-  // ---- P5: row index = rank of each clique vertex by (x, y, id): x-major grid columns
+  // ---- P5: row index = rank of each clique vertex by (x, y, id).  Counting sort of the
+  // vertices by a fine x bucket (n buckets over the x extent; monotone in x), then rank inside
+  // the bucket.  The grid arrays of P1 are dead: parent holds the bucket counters, scell the
+  // vertices (sorted positions) in bucket order.
   if (H.status == 0) {
-    const int gx = H.gx, gy = H.gy;
-    uint32_t* colc = S.parent;
-    for (int q = tid; q <= gx; q += FWG) colc[q] = 0;
+    uint32_t* bcnt = S.parent;
+    uint16_t* blist = S.scell;
+    const double minx = H.minx, xbs = H.xbs;
+    auto xbucket = [&](double xv) { return (int)fmin((xv - minx) * xbs, (double)(n - 1)); };
+    for (int q = tid; q <= n; q += FWG) bcnt[q] = 0;
     __syncthreads();
-    for (int t = tid; t < n; t += FWG)
-      if (S.smark[t]) atomicAdd(&colc[S.scell[t] / gy], 1u);
-    __syncthreads();
-    const int64_t V = block_scan_array<FWG>(colc, gx, H.red64);
-    if (tid == 0) H.V = (int)V;
-    // rank inside the x-major grid column by (x, y, id); lanes walk sorted positions, so a
-    // wave shares its column (same trip count, broadcast reads)
     for (int t = tid; t < n; t += FWG) {
       if (!S.smark[t]) continue;
-      const int cx = S.scell[t] / gy;
+      S.vrank[S.citems[t]] = (uint16_t)atomicAdd(&bcnt[xbucket(S.sxy[t].x)], 1u);
+    }
+    __syncthreads();
+    const int64_t V = block_scan_array<FWG>(bcnt, n, H.red64);
+    if (tid == 0) { H.V = (int)V; bcnt[n] = (uint32_t)V; }
+    for (int t = tid; t < n; t += FWG) {
+      if (!S.smark[t]) continue;
+      blist[bcnt[xbucket(S.sxy[t].x)] + S.vrank[S.citems[t]]] = (uint16_t)t;
+    }
+    __syncthreads();
+    for (int t = tid; t < n; t += FWG) {
+      if (!S.smark[t]) continue;
       const double2 v = S.sxy[t];
       const int vi = S.citems[t];
-      uint32_t rk = colc[cx];
-      const int lo = S.cstart[cx * gy], hi = S.cstart[(cx + 1) * gy];
+      const int b = xbucket(v.x);
+      const int lo = bcnt[b], hi = bcnt[b + 1];
+      uint32_t rk = lo;
       for (int u = lo; u < hi; ++u) {
-        const uint8_t mk = S.smark[u];
-        const double2 w = S.sxy[u];
-        const int ui = S.citems[u];
-        rk += mk && ((w.x < v.x) || (w.x == v.x && (w.y < v.y || (w.y == v.y && ui < vi))));
+        const int tu = blist[u];
+        const double2 w = S.sxy[tu];
+        const int ui = S.citems[tu];
+        rk += (w.x < v.x) || (w.x == v.x && (w.y < v.y || (w.y == v.y && ui < vi)));
       }
       S.vrank[vi] = (uint16_t)rk;
     }
@@ -730,34 +760,46 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
 
     STOP_AFTER(5);
     STAMP(11);
-    // ---- P6: stage the clique vertices' scores in LDS (the union region is dead now), then
-    // per chunk of <= cbuf_cap cliques: DFS fill of the member buffer (thread per root), then
-    // the ILP epilogue + COO rows with one thread per clique (coalesced output stores).
+    // ---- P6: stage the clique vertices' scores in LDS, then the ILP epilogue + COO rows with
+    // one thread per clique (coalesced output stores).  Cliques come from the P4 queue, whose
+    // output index is (root's scanned offset + ordinal within the root): the same order as a
+    // sequential root-by-root walk.  Micrographs whose cliques overflowed the queue re-walk
+    // the DFS per chunk of <= cbuf_cap cliques.
     for (int i = tid; i < n; i += FWG)
       if (S.flags[i] == 3) S.sscore[i] = c.score[b0 + i];
     __syncthreads();
     const int64_t Cm = H.C;
-    for (int64_t c0 = 0; c0 < Cm; c0 += cbuf_cap) {
-      const int64_t c1 = min(Cm, c0 + (int64_t)cbuf_cap);
-      c.c0 = c0;
-      c.c1 = c1;
-      for (int r = tid; r < n0; r += FWG) {
-        const int64_t lo = S.cnt[r], hi = S.cnt[r + 1];
-        if (lo == hi || hi <= c0 || lo >= c1) continue;
+    if (Cm <= c.cq_cap) {
+      for (int64_t sl = tid; sl < Cm; sl += FWG) {
         int mem[K];
-        mem[0] = r;
-        c.out = lo;
-        FLevel<K, 1, true>::run(c, mem);
-      }
-      __syncthreads();
-      for (int64_t j = c0 + tid; j < c1; j += FWG) {
-        int mem[K];
-        const uint16_t* sb = S.cbuf + (j - c0) * K;
+        const uint16_t* sb = S.cbuf + sl * K;
 #pragma unroll
         for (int i = 0; i < K; ++i) mem[i] = sb[i];
-        fused_epilogue<K>(c, H.base + j, mem);
+        fused_epilogue<K>(c, H.base + S.cnt[mem[0]] + c.cq_ord[sl], mem);
       }
-      __syncthreads();
+    } else {
+      for (int64_t c0 = 0; c0 < Cm; c0 += cbuf_cap) {
+        const int64_t c1 = min(Cm, c0 + (int64_t)cbuf_cap);
+        c.c0 = c0;
+        c.c1 = c1;
+        for (int r = tid; r < n0; r += FWG) {
+          const int64_t lo = S.cnt[r], hi = S.cnt[r + 1];
+          if (lo == hi || hi <= c0 || lo >= c1) continue;
+          int mem[K];
+          mem[0] = r;
+          c.out = lo;
+          FLevel<K, 1, true>::run(c, mem);
+        }
+        __syncthreads();
+        for (int64_t j = c0 + tid; j < c1; j += FWG) {
+          int mem[K];
+          const uint16_t* sb = S.cbuf + (j - c0) * K;
+#pragma unroll
+          for (int i = 0; i < K; ++i) mem[i] = sb[i];
+          fused_epilogue<K>(c, H.base + j, mem);
+        }
+        __syncthreads();
+      }
     }
   }
   STAMP(12);

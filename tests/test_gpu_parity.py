@@ -83,30 +83,23 @@ def _canon(rows, w, conf, cons_xyid):
             np.asarray(conf)[perm].view(np.uint32), [cons_xyid[i] for i in perm])
 
 
-@pytest.mark.parametrize("cfg_name,n_mg,get_cc,no_fused", [
-    ("C2", 24, False, False), ("C2", 8, True, False), ("C4", 6, False, False),
-    ("C2", 8, False, True), ("C3", 2, False, False), ("C3", 1, True, False)])
-def test_gpu_matches_oracle_synthetic(cfg_name, n_mg, get_cc, no_fused):
-    from repic_amd import _lib, synth
+def _check_vs_oracle(mgs, k, box, get_cc=False, no_fused=False):
+    from repic_amd import _lib
     from repic_amd.pipeline import Batch, run_batch
-    cfg = synth.SynthConfig(**synth.CONFIGS[cfg_name], seed=5, logit=(1,))
-    mgs = synth.batch(cfg, n_mg)
-    from repic_amd.ingest import sigmoid
-    mgs = [[(x, y, sigmoid(s) if s.min() < 0 else s) for (x, y, s) in mg] for mg in mgs]
-    batch = Batch.pack(cfg.k, cfg.box, mgs)
+    batch = Batch.pack(k, box, mgs)
     ctx = _lib.Context(0)
     res = run_batch(ctx, batch, get_cc=get_cc, no_fused=no_fused)
-    methods = [f"picker{p}" for p in range(cfg.k)]
+    methods = [f"picker{p}" for p in range(k)]
     for m, mg in enumerate(mgs):
-        o = _oracle_mg(mg, cfg.box, methods, int(batch.id_base[m]), get_cc)
+        o = _oracle_mg(mg, box, methods, int(batch.id_base[m]), get_cc)
         r = res[m]
         assert r.status == _lib.OK
         assert (r.cc_max, r.cc_cnt) == (o["cc_max"], o["cc_cnt"])
         A = o["A"].tocoo()
         C = A.shape[1]
-        orows = np.sort(A.row[np.argsort(A.col, kind="stable")].reshape(C, cfg.k), axis=1)
+        orows = np.sort(A.row[np.argsort(A.col, kind="stable")].reshape(C, k), axis=1)
         assert r.n_vert == A.shape[0] and len(r.w) == C
-        b0 = int(batch.box_off[m * cfg.k])
+        b0 = int(batch.box_off[m * k])
         idb = int(batch.id_base[m]) - b0
         gcons = [(float(batch.x[g]), float(batch.y[g]), idb + int(g)) for g in r.consensus]
         a = _canon(orows, o["w"], o["conf"], o["consensus"])
@@ -115,6 +108,41 @@ def test_gpu_matches_oracle_synthetic(cfg_name, n_mg, get_cc, no_fused):
         assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
         assert a[3] == b[3]
     ctx.close()
+
+
+@pytest.mark.parametrize("cfg_name,n_mg,get_cc,no_fused", [
+    ("C2", 24, False, False), ("C2", 8, True, False), ("C4", 6, False, False),
+    ("C2", 8, False, True), ("C3", 2, False, False), ("C3", 1, True, False)])
+def test_gpu_matches_oracle_synthetic(cfg_name, n_mg, get_cc, no_fused):
+    from repic_amd import synth
+    from repic_amd.ingest import sigmoid
+    cfg = synth.SynthConfig(**synth.CONFIGS[cfg_name], seed=5, logit=(1,))
+    mgs = synth.batch(cfg, n_mg)
+    mgs = [[(x, y, sigmoid(s) if s.min() < 0 else s) for (x, y, s) in mg] for mg in mgs]
+    _check_vs_oracle(mgs, cfg.k, cfg.box, get_cc, no_fused)
+
+
+def _dense_clusters(k, per, n_clusters, seed, box=100):
+    """Clusters of `per` near-duplicate boxes per picker: per**k cliques per cluster, far more
+    cliques than boxes (the fused kernel's clique queue overflows -> chunked DFS re-walk)."""
+    rng = np.random.default_rng(seed)
+    cx = rng.uniform(0, 3000, n_clusters).round()
+    cy = rng.uniform(0, 3000, n_clusters).round()
+    mg = []
+    for _ in range(k):
+        x = np.concatenate([c + rng.integers(-3, 4, per) for c in cx]).astype(np.float64)
+        y = np.concatenate([c + rng.integers(-3, 4, per) for c in cy]).astype(np.float64)
+        s = rng.uniform(0.3, 1.0, len(x))
+        mg.append((x, y, s))
+    return mg
+
+
+@pytest.mark.parametrize("k,per,n_clusters", [(3, 12, 3), (5, 4, 2), (8, 3, 1), (4, 2, 40)])
+def test_gpu_dense_clusters_match_oracle(k, per, n_clusters):
+    mgs = [_dense_clusters(k, per, n_clusters, seed) for seed in range(2)]
+    _check_vs_oracle(mgs, k, 100)
+    _check_vs_oracle(mgs, k, 100, get_cc=True)
+    _check_vs_oracle(mgs, k, 100, no_fused=True)
 
 
 def test_gpu_full_c2_properties():

@@ -2,7 +2,7 @@
 """Marginal cost of each fused-kernel phase: time the ablation builds (kernel stops after
 phase N) and the product build on the same batch, interleaved in one process.
 
-  make -C repic-copy_amd/csrc ablate && python tools/ablate.py [C2] [n_mg] [rounds]
+  make -C repic-copy_amd/csrc ablate && python tools/ablate.py [C2] [n_mg] [rounds] [lib.so]
 """
 import ctypes as C
 import glob
@@ -22,6 +22,8 @@ rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 7
 cfg = synth.SynthConfig(**synth.CONFIGS[cfg_name], seed=0)
 batch = Batch.pack(cfg.k, cfg.box, synth.batch(cfg, n_mg))
 libs = sorted(glob.glob(os.path.join(ROOT, "repic-copy_amd/repic_amd/ablate/*.so"))) + [_lib.LIB_PATH]
+if len(sys.argv) > 4:   # one library only (per-phase PMC passes: tools/gpu_pmc_ablate.sh)
+    libs = [sys.argv[4]]
 
 
 class Runner:
