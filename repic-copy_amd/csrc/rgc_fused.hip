@@ -32,10 +32,10 @@ struct FusedHdr {
   int64_t red64[FNW];
   uint64_t redu[FNW];
   int redi[FNW];
-  double minx, miny, cell;
+  double minx, miny, cell, inv_cell;
   double xbs;       // P5 x-bucket scale: bucket(x) = min(trunc((x - minx) * xbs), n - 1)
   float inv_gy;
-  int gx, gy, ncell;
+  int gx, gy, ncell, nkey;   // per-picker grid gx x gy; keys picker * ncell + cell; nkey = none
   int E, nodes, cc_cnt, cc_max, target, V, status;
   uint32_t ccur;    // P4 clique-queue cursor
   int64_t C, base;
@@ -165,11 +165,13 @@ __device__ __forceinline__ bool contains16(const uint16_t* a, int lo, int hi, in
   return p < hi && (int)a[p] == v;
 }
 
-__device__ __forceinline__ int cell_xm(const FusedHdr& H, double x, double y, int* cx, int* cy) {
-  if (H.ncell == 0 || !isfinite(x) || !isfinite(y)) return H.ncell;
-  *cx = (int)fmin(floor((x - H.minx) / H.cell), (double)(H.gx - 1));
-  *cy = (int)fmin(floor((y - H.miny) / H.cell), (double)(H.gy - 1));
-  return *cx * H.gy + *cy;
+// P1 sort key of a box of picker p: its cell in picker p's grid (x-major), or nkey when the
+// box cannot have an edge (non-finite coordinates).  Monotone in x and y per picker.
+__device__ __forceinline__ int box_key(const FusedHdr& H, int p, double x, double y) {
+  if (H.ncell == 0 || !isfinite(x) || !isfinite(y)) return H.nkey;
+  const int cx = (int)fmin(floor((x - H.minx) * H.inv_cell), (double)(H.gx - 1));
+  const int cy = (int)fmin(floor((y - H.miny) * H.inv_cell), (double)(H.gy - 1));
+  return p * H.ncell + cx * H.gy + cy;
 }
 
 // graph insertion key of a clique vertex (tiny graphs only): first appearance of the node in
@@ -297,38 +299,48 @@ struct FLevel<K, K, FILL> {
   }
 };
 
-// 3x3 stencil of a box (sorted position ts) as three column ranges of sorted positions.
+// Candidates of a box: the 3x3 cell stencil around its cell in the grid of every HIGHER
+// picker (forward edges only), i.e. up to 3 (K - 1 - p) column ranges of sorted positions.
 struct Stencil {
-  int i, pe, lo0, L0, lo1, L01, lo2, L;
+  int p, cx, y0, y1;   // p = K: no candidates
   double2 a;
 };
 
 template <int K>
 __device__ __forceinline__ void stencil_setup(Stencil& st, int ts, const FShared& S,
-                                              const FusedHdr& H, const int (&pb)[K + 1]) {
-  const int q = S.scell[ts];
-  st.i = S.citems[ts];
-  st.pe = picker_end<K>(pb, st.i);
+                                              const FusedHdr& H) {
+  const int key = S.scell[ts];
   st.a = S.sxy[ts];
-  st.lo0 = st.lo1 = st.lo2 = 0;
-  st.L0 = st.L01 = st.L = 0;
-  if (q >= H.ncell) return;
-  const int gy = H.gy;
-  // q / gy through a float reciprocal, corrected to the exact quotient (q < 2^16)
-  int cx = (int)((float)q * H.inv_gy);
-  cx += ((cx + 1) * gy <= q) ? 1 : 0;
-  cx -= (cx * gy > q) ? 1 : 0;
-  const int cy = q - cx * gy;
-  const int y0 = max(cy - 1, 0), y1 = min(cy + 1, gy - 1);
-  int l0 = 0, h0 = 0, l1, h1, l2 = 0, h2 = 0;
-  if (cx > 0) { l0 = S.cstart[(cx - 1) * gy + y0]; h0 = S.cstart[(cx - 1) * gy + y1 + 1]; }
-  l1 = S.cstart[cx * gy + y0];
-  h1 = S.cstart[cx * gy + y1 + 1];
-  if (cx + 1 < H.gx) { l2 = S.cstart[(cx + 1) * gy + y0]; h2 = S.cstart[(cx + 1) * gy + y1 + 1]; }
-  st.lo0 = l0; st.lo1 = l1; st.lo2 = l2;
-  st.L0 = h0 - l0;
-  st.L01 = st.L0 + (h1 - l1);
-  st.L = st.L01 + (h2 - l2);
+  st.p = K;
+  st.cx = 0;
+  st.y0 = 0;
+  st.y1 = -1;
+  if (key >= H.nkey) return;
+  const int gy = H.gy, nc = H.ncell;
+  // key / ncell and cell / gy through float reciprocals, corrected to the exact quotients
+  int p = 0;
+#pragma unroll
+  for (int q = 1; q < K; ++q) p += (key >= q * nc) ? 1 : 0;
+  const int cell = key - p * nc;
+  int cx = (int)((float)cell * H.inv_gy);
+  cx += ((cx + 1) * gy <= cell) ? 1 : 0;
+  cx -= (cx * gy > cell) ? 1 : 0;
+  const int cy = cell - cx * gy;
+  st.p = p;
+  st.cx = cx;
+  st.y0 = max(cy - 1, 0);
+  st.y1 = min(cy + 1, gy - 1);
+}
+
+// column range [lo, hi) of the stencil in picker q's grid, column offset d (-1, 0, 1)
+__device__ __forceinline__ void stencil_range(const Stencil& st, const FShared& S,
+                                              const FusedHdr& H, int q, int d, int& lo, int& hi) {
+  const int col = st.cx + d;
+  lo = hi = 0;
+  if (col < 0 || col >= H.gx) return;
+  const int cb = q * H.ncell + col * H.gy;
+  lo = S.cstart[cb + st.y0];
+  hi = S.cstart[cb + st.y1 + 1];
 }
 
 __device__ __forceinline__ bool edge_test(double2 a, double2 b, double B, double two_b2,
@@ -346,32 +358,25 @@ __device__ __forceinline__ bool edge_test(double2 a, double2 b, double B, double
   return inter / (two_b2 - inter) > 0.3;                      // reference quotient
 }
 
-// sorted position of stencil candidate kk (kk < st.L)
-__device__ __forceinline__ int stencil_pos(const Stencil& st, int kk) {
-  return kk < st.L0 ? st.lo0 + kk : (kk < st.L01 ? st.lo1 + (kk - st.L0) : st.lo2 + (kk - st.L01));
-}
-
 // P2 count for the box at sorted position ts (thread per box): JI test against every stencil
 // candidate of a higher picker; returns the edge count and the bitmask of edge candidates
-// (candidates 0..31; boxes with more candidates are re-tested by the fill).
+// (candidates 0..31 in stencil order; later candidates are re-tested by the fill).
 template <int K>
-__device__ __forceinline__ int pairs_count(const Stencil& st, const FShared& S, double B,
-                                           double two_b2, double i_lo, double i_hi,
+__device__ __forceinline__ int pairs_count(const Stencil& st, const FShared& S, const FusedHdr& H,
+                                           double B, double two_b2, double i_lo, double i_hi,
                                            uint32_t* mask_out) {
   uint32_t mask = 0;
-  int cnt = 0;
-  int kk = 0;
-  const int los[3] = {st.lo0, st.lo1, st.lo2};
-  const int lens[3] = {st.L0, st.L01 - st.L0, st.L - st.L01};
+  int cnt = 0, kk = 0;
+  for (int q = st.p + 1; q < K; ++q) {
 #pragma unroll
-  for (int r = 0; r < 3; ++r) {
-    const int lo = los[r], hi = los[r] + lens[r];
-    for (int t = lo; t < hi; ++t, ++kk) {
-      const int j = S.citems[t];
-      if (j < st.pe) continue;
-      if (edge_test(st.a, S.sxy[t], B, two_b2, i_lo, i_hi)) {
-        ++cnt;
-        mask |= (kk < 32) ? (1u << kk) : 0u;
+    for (int d = -1; d <= 1; ++d) {
+      int lo, hi;
+      stencil_range(st, S, H, q, d, lo, hi);
+      for (int t = lo; t < hi; ++t, ++kk) {
+        if (edge_test(st.a, S.sxy[t], B, two_b2, i_lo, i_hi)) {
+          ++cnt;
+          mask |= (kk < 32) ? (1u << kk) : 0u;
+        }
       }
     }
   }
@@ -379,26 +384,36 @@ __device__ __forceinline__ int pairs_count(const Stencil& st, const FShared& S, 
   return cnt;
 }
 
-// P2 fill: write the box's forward targets at dst[base..) from the count's bitmask (or by
-// re-testing), then sort them by target (insertion sort; lists are short).
+// P2 fill: write the box's forward targets at d[0..cnt) from the count's bitmask (re-testing
+// candidates past the 32nd), then sort them by target (insertion sort; lists are short).
 template <int K>
-__device__ __forceinline__ void pairs_fill(const Stencil& st, const FShared& S, uint32_t mask,
-                                           int base, int cnt, double B, double two_b2,
-                                           double i_lo, double i_hi) {
-  uint16_t* d = S.dst + base;
-  int c = 0;
-  if (st.L <= 32) {
-    while (mask) {
-      const int kk = __builtin_ctz(mask);
-      mask &= mask - 1;
-      d[c++] = S.citems[stencil_pos(st, kk)];
-    }
-  } else {
-    for (int kk = 0; kk < st.L; ++kk) {
-      const int t = stencil_pos(st, kk);
-      const int j = S.citems[t];
-      if (j < st.pe) continue;
-      if (edge_test(st.a, S.sxy[t], B, two_b2, i_lo, i_hi)) d[c++] = (uint16_t)j;
+__device__ __forceinline__ void pairs_fill(const Stencil& st, const FShared& S, const FusedHdr& H,
+                                           uint32_t mask, uint16_t* d, int cnt, double B,
+                                           double two_b2, double i_lo, double i_hi) {
+  int c = 0, kk = 0;
+  for (int q = st.p + 1; q < K; ++q) {
+#pragma unroll
+    for (int dd = -1; dd <= 1; ++dd) {
+      int lo, hi;
+      stencil_range(st, S, H, q, dd, lo, hi);
+      const int len = hi - lo;
+      if (kk + len <= 32) {
+        uint32_t bits = kk < 32 ? (mask >> kk) : 0u;
+        bits &= len >= 32 ? ~0u : ((1u << len) - 1u);
+        while (bits) {
+          const int b = __builtin_ctz(bits);
+          bits &= bits - 1;
+          d[c++] = S.citems[lo + b];
+        }
+      } else {
+        for (int t = lo; t < hi; ++t) {
+          const int idx = kk + (t - lo);
+          const bool e = idx < 32 ? ((mask >> idx) & 1u) != 0
+                                  : edge_test(st.a, S.sxy[t], B, two_b2, i_lo, i_hi);
+          if (e) d[c++] = S.citems[t];
+        }
+      }
+      kk += len;
     }
   }
   for (int a = 1; a < cnt; ++a) {
@@ -489,51 +504,53 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
 
   STOP_AFTER(0);
   STAMP(1);
-  // ---- P1: grid (x-major cells, at most 4n + 1 cells and n + 1 columns).  JI > 0.3 implies
-  // I > (6/13) B^2 and so |dx|, |dy| < (7/13) B = 0.5385 B: cells of side 0.54 B keep every
-  // edge inside the 3x3 stencil while the stencil area is 3.4x smaller than with side B.
+  // ---- P1: one grid per picker (x-major cells, K * gx * gy <= 4 nmax + 4 cells in all) and
+  // an LDS counting sort of the boxes by (picker, cell).  JI > 0.3 implies I > (6/13) B^2 and
+  // so |dx|, |dy| < (7/13) B = 0.5385 B: cells of side >= 0.54 B keep every edge inside the
+  // 3x3 stencil, and per-picker grids let a box visit the boxes of higher pickers only.
   if (tid == 0) {
-    H.minx = mnx; H.miny = mny; H.cell = A.B; H.gx = 0; H.gy = 0; H.ncell = 0;
+    H.minx = mnx; H.miny = mny; H.cell = A.B; H.inv_cell = 0.0; H.gx = 0; H.gy = 0; H.ncell = 0;
     H.status = 0; H.C = 0; H.base = 0; H.V = 0; H.target = -1; H.ccur = 0;
     if (mnx <= mxx && A.B > 0.0) {
       const double ex = mxx - mnx, ey = mxy - mny;
       if (!(ex < 0x1p40 && ey < 0x1p40)) {
         H.cell = INFINITY; H.gx = 1; H.gy = 1;
       } else {
-        double cl = 0.54 * A.B;
+        const double budget = (double)((4 * A.nmax + 4) / K);
+        double cl = fmax(0.54 * A.B, fmax(sqrt(ex * ey / budget), fmax(ex, ey) / budget));
         for (;;) {
           const double fx = floor(ex / cl) + 1.0, fy = floor(ey / cl) + 1.0;
-          if (fx * fy <= (double)(4 * n + 1) && fx <= (double)(n + 1)) {
+          if (fx * fy <= budget) {
             H.gx = (int)fx; H.gy = (int)fy;
             break;
           }
-          cl *= 2.0;
+          cl *= 1.0625;
         }
         H.cell = cl;
+        H.inv_cell = 1.0 / cl;
       }
       H.ncell = H.gx * H.gy;
     }
+    H.nkey = K * H.ncell;
     H.inv_gy = H.gy > 0 ? 1.0f / (float)H.gy : 0.0f;
     const double ex = mxx - mnx;
     H.xbs = (mnx < mxx && ex < 0x1p60) ? (double)n / ex : 0.0;
   }
   __syncthreads();
-  const int nc = H.ncell;
-  // counting sort by cell with packed u16 counters (two cells per LDS word)
+  const int nk = H.nkey;
+  // counting sort by key with packed u16 counters (two keys per LDS word)
   uint32_t* cw = reinterpret_cast<uint32_t*>(S.cstart);
-  for (int q = tid; q <= (nc + 2) / 2; q += FWG) cw[q] = 0;
+  for (int q = tid; q <= (nk + 2) / 2; q += FWG) cw[q] = 0;
   __syncthreads();
   for (int i = tid; i < n; i += FWG) {
-    int cx, cy;
-    const int q = cell_xm(H, A.x[b0 + i], A.y[b0 + i], &cx, &cy);
+    const int q = box_key(H, picker_of<K>(c.pb, i), A.x[b0 + i], A.y[b0 + i]);
     atomicAdd(&cw[q >> 1], 1u << (16 * (q & 1)));
   }
   __syncthreads();
-  block_scan_u16<FWG>(S.cstart, nc + 1, H.red64);
+  block_scan_u16<FWG>(S.cstart, nk + 1, H.red64);
   for (int i = tid; i < n; i += FWG) {
-    int cx, cy;
     const double xv = A.x[b0 + i], yv = A.y[b0 + i];
-    const int q = cell_xm(H, xv, yv, &cx, &cy);
+    const int q = box_key(H, picker_of<K>(c.pb, i), xv, yv);
     const int sh = 16 * (q & 1);
     const int t = (atomicAdd(&cw[q >> 1], 1u << sh) >> sh) & 0xFFFF;
     S.citems[t] = (uint16_t)i;
@@ -542,16 +559,16 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
     S.sxy[t] = make_double2(xv, yv);
   }
   __syncthreads();
-  // the cursors now hold cell ends: rebuild the starts from the sorted cell ids
+  // the cursors now hold key ends: rebuild the starts from the sorted keys
   for (int t = tid; t < n; t += FWG) {
     const int q = S.scell[t];
     const int qp = t ? (int)S.scell[t - 1] : -1;
     for (int qq = qp + 1; qq <= q; ++qq) S.cstart[qq] = (uint16_t)t;
     if (t == n - 1)
-      for (int qq = q + 1; qq <= nc + 1; ++qq) S.cstart[qq] = (uint16_t)n;
+      for (int qq = q + 1; qq <= nk + 1; ++qq) S.cstart[qq] = (uint16_t)n;
   }
   if (n == 0 && tid == 0)
-    for (int qq = 0; qq <= nc + 1; ++qq) S.cstart[qq] = 0;
+    for (int qq = 0; qq <= nk + 1; ++qq) S.cstart[qq] = 0;
   __syncthreads();
 
   STOP_AFTER(1);
@@ -565,14 +582,15 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
   // band moves the quotient by >= 1.1e-12 relative), so the decision is the reference's.
   const double t_star = 0.6 * B * B / 1.3;
   const double i_lo = t_star * (1.0 - 0x1p-40), i_hi = t_star * (1.0 + 0x1p-40);
-  // thread per box (sorted position): lanes of a wave hold neighbouring boxes, so their
-  // stencils overlap (similar trip counts, broadcast LDS reads).  cnt[] (dead until P3) keeps
+  // thread per box (sorted position): lanes of a wave hold neighbouring boxes of one picker,
+  // so their stencils overlap (similar trip counts, broadcast LDS reads), and the waves of
+  // picker K-1 have nothing to do.  cnt[] (dead until P3) keeps
   // each box's edge bitmask for the fill.
   for (int ts = tid; ts < n; ts += FWG) {
     Stencil st;
-    stencil_setup<K>(st, ts, S, H, c.pb);
+    stencil_setup<K>(st, ts, S, H);
     uint32_t mask;
-    S.fwd[st.i] = (uint32_t)pairs_count<K>(st, S, B, two_b2, i_lo, i_hi, &mask);
+    S.fwd[S.citems[ts]] = (uint32_t)pairs_count<K>(st, S, H, B, two_b2, i_lo, i_hi, &mask);
     S.cnt[ts] = mask;
   }
   __syncthreads();
@@ -590,9 +608,11 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
   if (H.status == 0) {
     for (int ts = tid; ts < n; ts += FWG) {
       Stencil st;
-      stencil_setup<K>(st, ts, S, H, c.pb);
-      const int base = S.fwd[st.i];
-      pairs_fill<K>(st, S, S.cnt[ts], base, (int)S.fwd[st.i + 1] - base, B, two_b2, i_lo, i_hi);
+      stencil_setup<K>(st, ts, S, H);
+      const int i = S.citems[ts];
+      const int base = S.fwd[i];
+      pairs_fill<K>(st, S, H, S.cnt[ts], S.dst + base, (int)S.fwd[i + 1] - base, B, two_b2,
+                    i_lo, i_hi);
     }
     __syncthreads();
     STAMP(6);
