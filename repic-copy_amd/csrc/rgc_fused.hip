@@ -594,8 +594,8 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
     S.cnt[ts] = mask;
   }
   __syncthreads();
-  STAMP(3);
-  STAMP(4);
+  STAMP(3);   // count
+  
   const int64_t E = block_scan_array<FWG>(S.fwd, n, H.red64);
   if (tid == 0) {
     S.fwd[n] = (uint32_t)E;
@@ -604,7 +604,7 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
     else if (E > A.ecap) H.status = RGC_ST_DEFER;
   }
   __syncthreads();
-  STAMP(5);
+  STAMP(4);   // scan
   if (H.status == 0) {
     for (int ts = tid; ts < n; ts += FWG) {
       Stencil st;
@@ -615,7 +615,7 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
                     i_lo, i_hi);
     }
     __syncthreads();
-    STAMP(6);
+    STAMP(5);   // fill + sort
   }
   if (H.status != 0) {
     if (tid == 0) {
@@ -629,7 +629,7 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
   }
 
   STOP_AFTER(2);
-  STAMP(7);
+  
   // ---- P3: connected components (union-find in LDS)
   for (int i = tid; i < n; i += FWG) {
     S.parent[i] = i;
@@ -656,6 +656,7 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
     }
   }
   __syncthreads();
+  STAMP(6);   // union
   for (int i = tid; i < n; i += FWG) {
     if (!S.flags[i]) continue;
     const uint32_t r = uf_find_lds(S.parent, i);
@@ -701,7 +702,7 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
   __syncthreads();
 
   STOP_AFTER(3);
-  STAMP(8);
+  STAMP(7);   // CC stats
   // ---- P4: clique count per picker-0 root, vertex marking, output reservation
   c.set_order = 2 * K < H.nodes;
   c.cq_cap = cbuf_bytes / (2 * K + 2);
@@ -721,7 +722,7 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
     S.cnt[r] = cntr;
   }
   __syncthreads();
-  STAMP(9);
+  STAMP(8);   // DFS
   const int64_t C = block_scan_array<FWG>(S.cnt, n0, H.red64);
   if (tid == 0) {
     S.cnt[n0] = (uint32_t)C;
@@ -737,7 +738,7 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
   __syncthreads();
 
   STOP_AFTER(4);
-  STAMP(10);
+  STAMP(9);   // scan + reserve
   // ---- P5: row index = rank of each clique vertex by (x, y, id).  Counting sort of the
   // vertices by a fine x bucket (n buckets over the x extent; monotone in x), then rank inside
   // the bucket.  The grid arrays of P1 are dead: parent holds the bucket counters, scell the
@@ -779,7 +780,7 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
     __syncthreads();
 
     STOP_AFTER(5);
-    STAMP(11);
+    STAMP(10);  // rank
     // ---- P6: stage the clique vertices' scores in LDS, then the ILP epilogue + COO rows with
     // one thread per clique (coalesced output stores).  Cliques come from the P4 queue, whose
     // output index is (root's scanned offset + ordinal within the root): the same order as a
@@ -788,6 +789,7 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
     for (int i = tid; i < n; i += FWG)
       if (S.flags[i] == 3) S.sscore[i] = c.score[b0 + i];
     __syncthreads();
+    STAMP(11);  // score staging
     const int64_t Cm = H.C;
     if (Cm <= c.cq_cap) {
       for (int64_t sl = tid; sl < Cm; sl += FWG) {

@@ -15,3 +15,8 @@ cat "$OUT/ablate.txt"
 timeout -k 10 200 python -u bench.py --config "$CFG" --n_mg "$NMG" --no-cpu-baseline \
   > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 1; }
 python -c "import json;d=json.load(open('$OUT/bench.json'));print(d['value'],d['pipeline']['kernel_ms'])"
+if [ -f repic-copy_amd/repic_amd/librepic_gc_diag.so ]; then
+  timeout -k 10 200 python -u tools/phase_stamps.py "$CFG" "$NMG" > "$OUT/stamps.txt" 2>&1 \
+    || { tail -20 "$OUT/stamps.txt"; exit 1; }
+  cat "$OUT/stamps.txt"
+fi
