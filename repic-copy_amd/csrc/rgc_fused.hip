@@ -26,12 +26,20 @@ namespace rgc {
 
 constexpr int FWG = 512;            // fused-kernel workgroup: 8 waves per micrograph
 constexpr int FNW = FWG / 64;
+constexpr int RB = 2;               // boxes per thread kept in registers from P0 to P1
 
 struct FusedHdr {
-  double redd[FNW];
-  int64_t red64[FNW];
-  uint64_t redu[FNW];
-  int redi[FNW];
+  // reduction scratch: the single-value reductions alias the 4-way one (every reduction
+  // starts behind a barrier)
+  union {
+    struct {
+      double redd[FNW];
+      int64_t red64[FNW];
+      uint64_t redu[FNW];
+      int redi[FNW];
+    };
+    double red4[4][FNW];
+  };
   double minx, miny, cell, inv_cell;
   double xbs;       // P5 x-bucket scale: bucket(x) = min(trunc((x - minx) * xbs), n - 1)
   float inv_gy;
@@ -343,19 +351,32 @@ __device__ __forceinline__ void stencil_range(const Stencil& st, const FShared& 
   hi = S.cstart[cb + st.y1 + 1];
 }
 
+// v_min_f64 / v_max_f64 without the sNaN canonicalisation fmin/fmax carry: grid candidates
+// have finite coordinates (non-finite boxes are never in a grid cell), where they equal
+// np.min / np.max
+__device__ __forceinline__ double min_f64(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double max_f64(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// JI > 0.3 (get_cliques.py:40-46, 64-65): branch-free overlap; the reference quotient is
+// evaluated only inside the ambiguity band [i_lo, i_hi] (rare, divergent)
 __device__ __forceinline__ bool edge_test(double2 a, double2 b, double B, double two_b2,
                                           double i_lo, double i_hi) {
-  // same values as np.min/np.max on finite coordinates (no NaN canonicalisation)
-  const bool lx = a.x < b.x, ly = a.y < b.y;
-  double xo = ((lx ? a.x : b.x) + B) - (lx ? b.x : a.x);
-  xo = xo > 0.0 ? xo : 0.0;
-  if (xo * B < i_lo) return false;                           // I <= xo * B
-  double yo = ((ly ? a.y : b.y) + B) - (ly ? b.y : a.y);
-  yo = yo > 0.0 ? yo : 0.0;
+  double xo = (min_f64(a.x, b.x) + B) - max_f64(a.x, b.x);
+  double yo = (min_f64(a.y, b.y) + B) - max_f64(a.y, b.y);
+  xo = max_f64(xo, 0.0);
+  yo = max_f64(yo, 0.0);
   const double inter = xo * yo;
-  if (inter > i_hi) return true;
-  if (inter < i_lo) return false;
-  return inter / (two_b2 - inter) > 0.3;                      // reference quotient
+  bool e = inter > i_hi;
+  if (!e && inter >= i_lo) e = inter / (two_b2 - inter) > 0.3;   // reference quotient
+  return e;
 }
 
 // P2 count for the box at sorted position ts (thread per box): JI test against every stencil
@@ -488,19 +509,49 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
   c.idb = A.id_base[m];
   const int n = c.n, b0 = c.b0;
 
-  // ---- P0: load coordinates, bounding box
+  // ---- P0: load coordinates (the first RB boxes of each thread stay in registers for P1),
+  // bounding box (one combined workgroup reduction)
+  double rx[RB], ry[RB];
+#pragma unroll
+  for (int j = 0; j < RB; ++j) {
+    const int i = tid + j * FWG;
+    rx[j] = i < n ? A.x[b0 + i] : 0.0;
+    ry[j] = i < n ? A.y[b0 + i] : 0.0;
+  }
+  // fn(i, x, y) for every box of this thread
+  auto each_box = [&](auto&& fn) {
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+      const int i = tid + j * FWG;
+      if (i < n) fn(i, rx[j], ry[j]);
+    }
+    for (int i = tid + RB * FWG; i < n; i += FWG) fn(i, A.x[b0 + i], A.y[b0 + i]);
+  };
   double mnx = INFINITY, mny = INFINITY, mxx = -INFINITY, mxy = -INFINITY;
-  for (int i = tid; i < n; i += FWG) {
-    const double xv = A.x[b0 + i], yv = A.y[b0 + i];
+  each_box([&](int, double xv, double yv) {
     if (isfinite(xv) && isfinite(yv)) {
       mnx = fmin(mnx, xv); mxx = fmax(mxx, xv);
       mny = fmin(mny, yv); mxy = fmax(mxy, yv);
     }
+  });
+  {
+    double v[4] = {mnx, mny, -mxx, -mxy};
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = fmin(v[r], __shfl_xor(v[r], o, 64));
+    if ((tid & 63) == 0)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) H.red4[r][tid >> 6] = v[r];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v[r] = H.red4[r][0];
+#pragma unroll
+      for (int w = 1; w < FNW; ++w) v[r] = fmin(v[r], H.red4[r][w]);
+    }
+    mnx = v[0]; mny = v[1]; mxx = -v[2]; mxy = -v[3];
   }
-  mnx = block_min<FWG>(mnx, H.redd);
-  mny = block_min<FWG>(mny, H.redd);
-  mxx = block_max<FWG>(mxx, H.redd);
-  mxy = block_max<FWG>(mxy, H.redd);
 
   STOP_AFTER(0);
   STAMP(1);
@@ -541,15 +592,23 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
   // counting sort by key with packed u16 counters (two keys per LDS word)
   uint32_t* cw = reinterpret_cast<uint32_t*>(S.cstart);
   for (int q = tid; q <= (nk + 2) / 2; q += FWG) cw[q] = 0;
-  __syncthreads();
+  // union-find / node flags / CC-size counters for the P2 fill (parent, flags, smark and vrank
+  // are untouched until then)
+  uint32_t* ccsz = reinterpret_cast<uint32_t*>(S.vrank);   // packed u16 CC sizes
   for (int i = tid; i < n; i += FWG) {
-    const int q = box_key(H, picker_of<K>(c.pb, i), A.x[b0 + i], A.y[b0 + i]);
-    atomicAdd(&cw[q >> 1], 1u << (16 * (q & 1)));
+    S.parent[i] = i;
+    S.flags[i] = 0;
+    S.smark[i] = 0;
   }
+  for (int q = tid; q < (n + 1) / 2; q += FWG) ccsz[q] = 0;
+  __syncthreads();
+  each_box([&](int i, double xv, double yv) {
+    const int q = box_key(H, picker_of<K>(c.pb, i), xv, yv);
+    atomicAdd(&cw[q >> 1], 1u << (16 * (q & 1)));
+  });
   __syncthreads();
   block_scan_u16<FWG>(S.cstart, nk + 1, H.red64);
-  for (int i = tid; i < n; i += FWG) {
-    const double xv = A.x[b0 + i], yv = A.y[b0 + i];
+  each_box([&](int i, double xv, double yv) {
     const int q = box_key(H, picker_of<K>(c.pb, i), xv, yv);
     const int sh = 16 * (q & 1);
     const int t = (atomicAdd(&cw[q >> 1], 1u << sh) >> sh) & 0xFFFF;
@@ -557,7 +616,7 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
     S.pos[i] = (uint16_t)t;
     S.scell[t] = (uint16_t)q;
     S.sxy[t] = make_double2(xv, yv);
-  }
+  });
   __syncthreads();
   // the cursors now hold key ends: rebuild the starts from the sorted keys
   for (int t = tid; t < n; t += FWG) {
@@ -606,13 +665,28 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
   __syncthreads();
   STAMP(4);   // scan
   if (H.status == 0) {
+    // fill + sort each list, then union its edges (lock-free union-find, P3's first half)
     for (int ts = tid; ts < n; ts += FWG) {
+      const int i = S.citems[ts];
+      const int base = S.fwd[i], cnt = (int)S.fwd[i + 1] - base;
+      if (cnt == 0) continue;
       Stencil st;
       stencil_setup<K>(st, ts, S, H);
-      const int i = S.citems[ts];
-      const int base = S.fwd[i];
-      pairs_fill<K>(st, S, H, S.cnt[ts], S.dst + base, (int)S.fwd[i + 1] - base, B, two_b2,
-                    i_lo, i_hi);
+      uint16_t* d = S.dst + base;
+      pairs_fill<K>(st, S, H, S.cnt[ts], d, cnt, B, two_b2, i_lo, i_hi);
+      S.flags[i] = 1;
+      for (int e = 0; e < cnt; ++e) {
+        const uint32_t h = d[e];
+        S.flags[h] = 1;
+        uint32_t a = i, b = h;
+        for (;;) {
+          a = uf_find_lds(S.parent, a);
+          b = uf_find_lds(S.parent, b);
+          if (a == b) break;
+          if (a < b) { const uint32_t t = a; a = b; b = t; }
+          if (atomicCAS(&S.parent[a], a, b) == a) break;
+        }
+      }
     }
     __syncthreads();
     STAMP(5);   // fill + sort
@@ -630,64 +704,50 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
 
   STOP_AFTER(2);
   
-  // ---- P3: connected components (union-find in LDS)
-  for (int i = tid; i < n; i += FWG) {
-    S.parent[i] = i;
-    S.flags[i] = 0;
-    S.smark[i] = 0;
-    S.cnt[i] = 0;
-  }
-  __syncthreads();
-  for (int i = tid; i < n; i += FWG) {
-    const int e0 = S.fwd[i], e1 = S.fwd[i + 1];
-    if (e0 == e1) continue;
-    S.flags[i] = 1;
-    for (int e = e0; e < e1; ++e) {
-      const uint32_t h = S.dst[e];
-      S.flags[h] = 1;
-      uint32_t a = i, b = h;
-      for (;;) {
-        a = uf_find_lds(S.parent, a);
-        b = uf_find_lds(S.parent, b);
-        if (a == b) break;
-        if (a < b) { const uint32_t t = a; a = b; b = t; }
-        if (atomicCAS(&S.parent[a], a, b) == a) break;
-      }
-    }
-  }
-  __syncthreads();
-  STAMP(6);   // union
+  // ---- P3: connected components: the unions ran in the P2 fill; compress, count sizes
+  STAMP(6);   // (empty: union fused into the fill)
   for (int i = tid; i < n; i += FWG) {
     if (!S.flags[i]) continue;
     const uint32_t r = uf_find_lds(S.parent, i);
     lds_st(S.parent + i, r);
-    atomicAdd(&S.cnt[r], 1u);
+    atomicAdd(&ccsz[r >> 1], 1u << (16 * (r & 1)));
   }
   __syncthreads();
+  auto cc_size = [&](uint32_t r) { return (int)((ccsz[r >> 1] >> (16 * (r & 1))) & 0xFFFF); };
   {
-    int64_t nodes = 0, roots = 0;
+    // nodes and roots packed in one 64-bit sum, the largest size in one max
+    int64_t nr = 0;
     int mx = 0;
     for (int i = tid; i < n; i += FWG) {
       if (S.flags[i]) {
-        ++nodes;
-        if (S.parent[i] == (uint32_t)i) { ++roots; mx = max(mx, (int)S.cnt[i]); }
+        nr += 1LL << 32;
+        if (S.parent[i] == (uint32_t)i) { nr += 1; mx = max(mx, cc_size(i)); }
       }
     }
-    nodes = block_sum64<FWG>(nodes, H.red64);
-    roots = block_sum64<FWG>(roots, H.red64);
-    mx = block_max_i<FWG>(mx, H.redi);
-    if (tid == 0) { H.nodes = (int)nodes; H.cc_cnt = (int)roots; H.cc_max = mx; }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      nr += __shfl_xor(nr, o, 64);
+      mx = max(mx, __shfl_xor(mx, o, 64));
+    }
+    if ((tid & 63) == 0) { H.red64[tid >> 6] = nr; H.redi[tid >> 6] = mx; }
+    __syncthreads();
+    if (tid == 0) {
+      int64_t t = 0;
+      int m2 = 0;
+      for (int w = 0; w < FNW; ++w) { t += H.red64[w]; m2 = max(m2, H.redi[w]); }
+      H.nodes = (int)(t >> 32); H.cc_cnt = (int)(t & 0xFFFFFFFF); H.cc_max = m2;
+    }
+    __syncthreads();
   }
   const bool get_cc = (A.flags & 1) != 0;
   if (get_cc) {
     // largest CC; ties -> the component whose first edge comes first in the enumeration
-    __syncthreads();
     uint64_t best = ~0ULL;
     for (int i = tid; i < n; i += FWG) {
       const int e0 = S.fwd[i], e1 = S.fwd[i + 1];
       if (e0 == e1) continue;
       const uint32_t r = S.parent[i];
-      if ((int)S.cnt[r] != H.cc_max) continue;
+      if (cc_size(r) != H.cc_max) continue;
       const int pi = picker_of<K>(c.pb, i);
       const int h = S.dst[e0];   // lists are sorted: the first target is the smallest key
       const int ph = picker_of<K>(c.pb, h);
