@@ -17,6 +17,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <vector>
 
 #include "../../include/repic_gc.h"
@@ -67,12 +70,69 @@ struct Buf {
   size_t cap = 0;
 };
 
-// Fused size classes: boxes per micrograph and forward-edge capacity per class.
-// (LDS bytes ~ 46 n + 2 ecap: class 1024 with ecap 3n fits 3 workgroups per CU, the top class
-// fills the 160 KiB of one CU)
-constexpr int N_CLASSES = 5;
-constexpr int CLASS_N[N_CLASSES] = {256, 512, 1024, 2048, 3000};
-constexpr int CLASS_E[N_CLASSES] = {4 * 256, 4 * 512, 3 * 1024, 4 * 2048, 4 * 3000};
+// LDS is allocated in 1280-byte blocks, 128 per CU (gfx950, measured with
+// tools/probe/lds_occ.hip: 3 workgroups per CU up to 53760 B, 2 above it; the HIP occupancy
+// API over-reports 3 up to 54613 B, so it is not used).
+constexpr int LDS_BLOCK = 1280;
+constexpr int LDS_BLOCKS = 128;
+constexpr int FUSED_WG = 512;
+static int lds_blocks(int bytes) { return (bytes + LDS_BLOCK - 1) / LDS_BLOCK; }
+
+// One fused launch configuration: micrographs of <= nmax boxes, forward-edge capacity ecap,
+// dynamic LDS bytes, coordinate width.
+struct FusedPlan {
+  int nmax = 0, ecap = 0, lds = 0;
+  bool wide = false;
+};
+
+// Workgroups per CU the kernel's VGPRs allow (8 waves per workgroup, 4 SIMDs, 512 VGPRs).
+static int vgpr_wg_cap(int k, bool wide) {
+  static int cache[2][MAX_K + 1] = {};
+  int& v = cache[wide][k];
+  if (!v) {
+    const int r = fused_vgprs(k, wide);
+    const int waves = r > 0 ? std::min(8, 512 / (((r + 7) / 8) * 8)) : 1;
+    v = std::max(1, waves * 4 / (FUSED_WG / 64));
+  }
+  return v;
+}
+
+// The most workgroups per CU that LDS (with ecap >= nmax) and VGPRs allow, then the largest
+// edge capacity at that occupancy (free LDS up to the next allocation boundary).
+// max_wg = 1: the whole 160 KiB (largest ecap).
+static bool plan_fused(int k, bool wide, int nmax, int max_wg, FusedPlan* p) {
+  const int base = fused_lds_bytes(nmax, 0, wide);
+  const int need = lds_blocks(fused_lds_bytes(nmax, nmax, wide));
+  if (need > LDS_BLOCKS) return false;
+  const int w = std::min(std::min(max_wg, vgpr_wg_cap(k, wide)), LDS_BLOCKS / need);
+  const int budget = (LDS_BLOCKS / w) * LDS_BLOCK;
+  int ecap = std::min(65535, (budget - base) / 2);
+  while (ecap > nmax && fused_lds_bytes(nmax, ecap, wide) > budget) ecap -= 8;
+  p->nmax = nmax;
+  p->ecap = ecap;
+  p->wide = wide;
+  p->lds = fused_lds_bytes(nmax, ecap, wide);
+  return p->lds <= budget;
+}
+
+// size class of a micrograph of n boxes (64-box steps to 1024, then 128, then 256)
+static int fused_class(int64_t n) {
+  if (n <= 1024) return (int)std::max<int64_t>(64, (n + 63) / 64 * 64);
+  if (n <= 2048) return (int)((n + 127) / 128 * 128);
+  return (int)((n + 255) / 256 * 256);
+}
+
+// plan_fused memoised per (k, pass, class); nmax = 0 marks "does not fit"
+static const FusedPlan& cached_plan(int k, int pass, int nmax) {
+  static std::map<std::tuple<int, int, int>, FusedPlan> memo;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = memo.find({k, pass, nmax});
+  if (it != memo.end()) return it->second;
+  FusedPlan p;
+  if (!plan_fused(k, pass > 0, nmax, pass == 2 ? 1 : LDS_BLOCKS, &p)) p = FusedPlan();
+  return memo.emplace(std::make_tuple(k, pass, nmax), p).first->second;
+}
 
 }  // namespace
 
@@ -363,27 +423,11 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   }
   hipStream_t s = c->stream;
 
-  // ---- classify micrographs
-  std::vector<int32_t> cls_list[N_CLASSES];
-  std::vector<int32_t> big;
-  const bool no_fused = (flags & RGC_F_NO_FUSED) != 0;
-  for (int q = 0; q < N_CLASSES; ++q)
-    if (fused_lds_bytes(CLASS_N[q], CLASS_E[q]) > 160 * 1024) return fail("internal: LDS class");
-  for (int m = 0; m < n_mg; ++m) {
-    const int64_t nm = in->box_off[(int64_t)(m + 1) * k] - in->box_off[(int64_t)m * k];
-    int cl = -1;
-    if (!no_fused)
-      for (int q = 0; q < N_CLASSES; ++q)
-        if (nm <= CLASS_N[q]) { cl = q; break; }
-    if (cl < 0) big.push_back(m);
-    else cls_list[cl].push_back(m);
-  }
-  const int n_fused = n_mg - (int)big.size();
-
   // ---- inputs on device
+  const bool no_fused = (flags & RGC_F_NO_FUSED) != 0;
   const double *x = in->x, *y = in->y, *sc = in->score;
   const size_t nbo = (size_t)n_mg * k + 1;
-  const size_t fstage = nbo * 4 + n_mg * 8 + n_mg * 4 + 64;
+  const size_t fstage = nbo * 4 + n_mg * 8 + 3 * (size_t)n_mg * 4 + 64;   // 3 passes of lists
   TRY(ensure_host(c, H_FSTAGE, fstage));
   int32_t* f_bo = H<int32_t>(c, H_FSTAGE);
   int64_t* f_id = reinterpret_cast<int64_t*>(
@@ -391,14 +435,9 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   int32_t* f_ml = reinterpret_cast<int32_t*>(f_id + n_mg);
   for (size_t i = 0; i < nbo; ++i) f_bo[i] = (int32_t)in->box_off[i];
   std::memcpy(f_id, in->id_base, n_mg * 8);
-  {
-    int o = 0;
-    for (int q = 0; q < N_CLASSES; ++q)
-      for (int32_t m : cls_list[q]) f_ml[o++] = m;
-  }
   TRY(ensure_dev(c, D_FBOXOFF, nbo * 4));
   TRY(ensure_dev(c, D_FIDBASE, n_mg * 8));
-  TRY(ensure_dev(c, D_MGLIST, n_mg * 4 + 4));
+  TRY(ensure_dev(c, D_MGLIST, 3 * (size_t)n_mg * 4 + 4));
   TRY(ensure_dev(c, D_FSTAT, n_mg * sizeof(MgStat)));
   TRY(ensure_dev(c, D_CURSOR, 16));
   TRY(ensure_host(c, H_FSTAT, n_mg * sizeof(MgStat)));
@@ -406,7 +445,6 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   TRY(mark(c, "h2d_meta"));
   HIPCHK(hipMemcpyAsync(D<void>(c, D_FBOXOFF), f_bo, nbo * 4, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(D<void>(c, D_FIDBASE), f_id, n_mg * 8, hipMemcpyHostToDevice, s));
-  if (n_fused) HIPCHK(hipMemcpyAsync(D<void>(c, D_MGLIST), f_ml, n_fused * 4, hipMemcpyHostToDevice, s));
   if (!(flags & RGC_F_DEVICE_INPUTS)) {
     TRY(ensure_dev(c, D_X, N * 8));
     TRY(ensure_dev(c, D_Y, N * 8));
@@ -419,11 +457,32 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
     sc = D<double>(c, D_S);
   }
 
+  // ---- fused passes.  Pass 0: f32-coordinate layout at the best occupancy; pass 1: the
+  // micrographs it deferred (coordinates not exact in f32, or more edges than its ecap) with
+  // f64 coordinates; pass 2: the edge-capacity overflows of pass 1 with the whole LDS.  What
+  // is still deferred (or too large for LDS) runs through the multi-kernel path.
   std::vector<MgStat> st(n_mg);
   int64_t fused_total = 0;
   int64_t E_total = 0;
-  std::vector<int32_t> deferred = big;
-  if (n_fused) {
+  std::vector<int32_t> deferred;
+  std::vector<int32_t> todo0;
+  std::vector<int32_t> mg_class(n_mg);
+  // per-call plan lookup: few distinct classes, so a linear list beats the shared memo
+  std::vector<std::pair<int, const FusedPlan*>> local_plans;
+  auto plan_of = [&](int pass, int cl) -> const FusedPlan& {
+    const int key = cl * 4 + pass;
+    for (const auto& lp : local_plans)
+      if (lp.first == key) return *lp.second;
+    local_plans.push_back({key, &cached_plan(k, pass, cl)});
+    return *local_plans.back().second;
+  };
+  for (int m = 0; m < n_mg; ++m) {
+    const int64_t nm = in->box_off[(int64_t)(m + 1) * k] - in->box_off[(int64_t)m * k];
+    mg_class[m] = nm <= 65535 ? fused_class(nm) : 0;
+    if (!no_fused && mg_class[m] && plan_of(0, mg_class[m]).nmax) todo0.push_back(m);
+    else deferred.push_back(m);
+  }
+  if (!todo0.empty()) {
     if (c->cap_cliques < 4096) c->cap_cliques = std::max<int64_t>(4096, N);
     for (int attempt = 0; attempt < 2; ++attempt) {
       TRY(ensure_outputs(c, c->cap_cliques, 0, k, want_members, multi != 0));
@@ -440,48 +499,86 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
       A.order = multi ? D<uint8_t>(c, D_ORDER) : nullptr;
       A.stamps = nullptr;
 #ifdef RGC_STAMPS
-      TRY(ensure_dev(c, D_STAMPS, (size_t)n_fused * 16 * 8));
-      HIPCHK(hipMemsetAsync(D<void>(c, D_STAMPS), 0, (size_t)n_fused * 128, s));
+      TRY(ensure_dev(c, D_STAMPS, 3 * (size_t)n_mg * 16 * 8));
+      HIPCHK(hipMemsetAsync(D<void>(c, D_STAMPS), 0, 3 * (size_t)n_mg * 128, s));
 #endif
-      int o = 0;
-      for (int q = 0; q < N_CLASSES; ++q) {
-        const int nb = (int)cls_list[q].size();
-        if (!nb) continue;
-        A.nmax = CLASS_N[q];
-        A.ecap = CLASS_E[q];
-        A.mg_list = D<int32_t>(c, D_MGLIST) + o;
+      std::vector<int32_t> todo = todo0, left;
+      int ml_off = 0;   // mg-list slots used (earlier passes' lists stay intact)
+      bool overflow = false;
+      for (int pass = 0; pass < 3 && !todo.empty(); ++pass) {
+        const bool wide = pass > 0;
+        // bucket by size class (few classes: linear search of the bucket keys)
+        std::vector<int> keys;
+        std::vector<std::vector<int32_t>> lists;
+        left.clear();
+        int last = -1;
+        for (int32_t m : todo) {
+          const int cl = mg_class[m];
+          if (!cl || !plan_of(pass, cl).nmax) { left.push_back(m); continue; }
+          if (last < 0 || keys[last] != cl) {
+            last = -1;
+            for (size_t q = 0; q < keys.size(); ++q)
+              if (keys[q] == cl) last = (int)q;
+            if (last < 0) { keys.push_back(cl); lists.emplace_back(); last = (int)keys.size() - 1; }
+          }
+          lists[last].push_back(m);
+        }
+        std::vector<int32_t> by;
+        std::vector<size_t> starts;
+        for (size_t q = 0; q < keys.size(); ++q) {
+          starts.push_back(by.size());
+          by.insert(by.end(), lists[q].begin(), lists[q].end());
+        }
+        std::memcpy(f_ml + ml_off, by.data(), by.size() * 4);
+        if (!by.empty())
+          HIPCHK(hipMemcpyAsync(D<int32_t>(c, D_MGLIST) + ml_off, f_ml + ml_off, by.size() * 4,
+                                hipMemcpyHostToDevice, s));
+        for (size_t q = 0; q < keys.size(); ++q) {
+          const FusedPlan& pl = plan_of(pass, keys[q]);
+          A.nmax = pl.nmax;
+          A.ecap = pl.ecap;
+          A.mg_list = D<int32_t>(c, D_MGLIST) + ml_off + starts[q];
 #ifdef RGC_STAMPS
-        A.stamps = D<unsigned long long>(c, D_STAMPS) + (size_t)o * 16;
+          A.stamps = D<unsigned long long>(c, D_STAMPS) + (size_t)(ml_off + starts[q]) * 16;
 #endif
-        TRY(mark(c, "k_fused"));
-        if (launch_fused(s, nb, fused_lds_bytes(A.nmax, A.ecap), A) != 0)
-          return fail("fused kernel launch failed");
-        o += nb;
+          TRY(mark(c, "k_fused"));
+          if (launch_fused(s, (int)lists[q].size(), pl.lds, A, wide) != 0)
+            return fail("fused kernel launch failed");
+        }
+        TRY(mark(c, "d2h_stats"));
+        HIPCHK(hipMemcpyAsync(H<void>(c, H_FSTAT), D<void>(c, D_FSTAT), n_mg * sizeof(MgStat),
+                              hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(H<void>(c, H_TOTAL), D<void>(c, D_CURSOR), 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(s));
+        const MgStat* fs = H<MgStat>(c, H_FSTAT);
+        ml_off += (int)by.size();
+        todo.clear();
+        for (const int32_t m : by) {
+          st[m] = fs[m];
+          if (fs[m].status == RGC_ST_OVERFLOW) overflow = true;
+          else if (fs[m].status == RGC_ST_DEFER_WIDE || fs[m].status == RGC_ST_DEFER) todo.push_back(m);
+        }
+        for (int32_t m : left) todo.push_back(m);
       }
-      TRY(mark(c, "d2h_stats"));
-      HIPCHK(hipMemcpyAsync(H<void>(c, H_FSTAT), D<void>(c, D_FSTAT), n_mg * sizeof(MgStat),
-                            hipMemcpyDeviceToHost, s));
-      HIPCHK(hipMemcpyAsync(H<void>(c, H_TOTAL), D<void>(c, D_CURSOR), 8, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipGetLastError());
-      HIPCHK(hipStreamSynchronize(s));
       fused_total = (int64_t)H<unsigned long long>(c, H_TOTAL)[0];
 #ifdef RGC_STAMPS
-      c->stamps.resize((size_t)n_fused * 16);
-      HIPCHK(hipMemcpy(c->stamps.data(), D<void>(c, D_STAMPS), (size_t)n_fused * 128,
+      c->stamps.resize((size_t)todo0.size() * 16);   // pass 0's workgroups
+      HIPCHK(hipMemcpy(c->stamps.data(), D<void>(c, D_STAMPS), todo0.size() * 128,
                        hipMemcpyDeviceToHost));
 #endif
-      if (fused_total <= c->cap_cliques) break;
+      if (!overflow && fused_total <= c->cap_cliques) {
+        for (int32_t m : todo) deferred.push_back(m);
+        break;
+      }
+      if (attempt == 1) return fail("internal: output overflow after regrow");
       c->cap_cliques = fused_total + fused_total / 8 + 1024;   // grow and re-run once
       c->n_ev = 0;
     }
-    const MgStat* fs = H<MgStat>(c, H_FSTAT);
-    for (int q = 0; q < N_CLASSES; ++q)
-      for (int32_t m : cls_list[q]) {
-        st[m] = fs[m];
-        if (fs[m].status == RGC_ST_OVERFLOW) return fail("internal: output overflow after regrow");
-        if (fs[m].status == RGC_ST_DEFER) deferred.push_back(m);
-        else E_total += fs[m].n_edges;
-      }
+    for (int32_t m : todo0) {
+      const int stt = st[m].status;
+      if (stt != RGC_ST_DEFER && stt != RGC_ST_DEFER_WIDE) E_total += st[m].n_edges;
+    }
   }
 
   int64_t C_total = fused_total;

@@ -49,14 +49,16 @@ struct FusedHdr {
   int64_t C, base;
 };
 
-__host__ __device__ inline FusedLayout fused_layout(int nmax, int ecap) {
+// wide: f64 coordinates in LDS; otherwise f32 (every coordinate of the micrograph is exactly
+// representable as f32, checked in P0, so the f64 values are recovered exactly)
+__host__ __device__ inline FusedLayout fused_layout(int nmax, int ecap, bool wide) {
   FusedLayout L;
   auto al = [](int v) { return (v + 15) & ~15; };
   int o = al((int)sizeof(FusedHdr));
   // live until the end of the kernel
-  L.off_sxy = o; o += al(16 * nmax);          // (x, y) in cell-sorted order
+  L.off_sxy = o; o += al((wide ? 16 : 8) * nmax);   // (x, y) in cell-sorted order
   L.off_cnt = o; o += al(4 * (nmax + 4));
-  L.off_fwd = o; o += al(4 * (nmax + 4));
+  L.off_fwd = o; o += al(2 * (nmax + 4));     // u16 CSR offsets (E <= ecap <= 65535)
   L.off_pos = o; o += al(2 * nmax);           // local box index -> sorted position
   L.off_vrank = o; o += al(2 * nmax);
   L.off_dst = o; o += al(2 * ecap);
@@ -67,31 +69,45 @@ __host__ __device__ inline FusedLayout fused_layout(int nmax, int ecap) {
   L.off_parent = o; o += al(4 * (nmax + 4));
   L.off_citems = o; o += al(2 * nmax);        // sorted position -> local box index
   L.off_scell = o; o += al(2 * nmax);         // sorted position -> cell
-  L.off_flags = o; o += al(nmax);             // by local index
-  L.off_smark = o; o += al(nmax);             // clique-vertex mark by sorted position
+  L.off_flags = o; o += al(nmax);             // by local index: 1 graph node, 3 clique vertex
+  L.off_smark = o;
   L.total = o;
   L.off_cbuf = L.off_cstart;
   return L;
 }
 
-int fused_lds_bytes(int nmax, int ecap) { return fused_layout(nmax, ecap).total; }
+int fused_lds_bytes(int nmax, int ecap, bool wide) { return fused_layout(nmax, ecap, wide).total; }
 
 struct FShared {
-  double2* sxy;     // cell-sorted coordinates
+  void* sxy;        // cell-sorted coordinates: double2 (wide) or float2
   uint16_t* cstart;
   uint32_t* cnt;
-  uint32_t* fwd;
+  uint16_t* fwd;
   uint32_t* parent;
   uint16_t* citems;
   uint16_t* pos;
   uint16_t* scell;
   uint16_t* vrank;
   uint8_t* flags;   // by local index: 0 no edge, 1 graph node, 3 clique vertex
-  uint8_t* smark;   // by sorted position: 1 clique vertex
   uint16_t* dst;
   double* sscore;   // P6 only (parent..scell): scores of clique vertices by local index
   uint16_t* cbuf;   // P4-P6 (cell starts): clique queue, or the current chunk of the re-walk
 };
+
+template <bool W>
+__device__ __forceinline__ double2 ld_xy(const FShared& S, int t) {
+  if constexpr (W) {
+    return reinterpret_cast<const double2*>(S.sxy)[t];
+  } else {
+    const float2 f = reinterpret_cast<const float2*>(S.sxy)[t];
+    return make_double2((double)f.x, (double)f.y);
+  }
+}
+template <bool W>
+__device__ __forceinline__ void st_xy(const FShared& S, int t, double x, double y) {
+  if constexpr (W) reinterpret_cast<double2*>(S.sxy)[t] = make_double2(x, y);
+  else reinterpret_cast<float2*>(S.sxy)[t] = make_float2((float)x, (float)y);
+}
 
 template <int K>
 struct FCtx {
@@ -204,14 +220,14 @@ __device__ __forceinline__ uint64_t ins_key(const FCtx<K>& c, int u) {
 
 // ILP epilogue of one buffered clique (thread per clique): reference get_cliques.py:169-202.
 // j = output index; mem = local box indices in picker order.  Scores come from LDS.
-template <int K>
+template <int K, bool W>
 __device__ __forceinline__ void fused_epilogue(const FCtx<K>& c, int64_t j, const int (&mem)[K]) {
   double ji[K][K], s[K], xs[K], ys[K];
   int64_t ids[K];
   uint64_t ins[K] = {};
 #pragma unroll
   for (int i = 0; i < K; ++i) {
-    const double2 xy = c.S.sxy[c.S.pos[mem[i]]];
+    const double2 xy = ld_xy<W>(c.S, c.S.pos[mem[i]]);
     xs[i] = xy.x;
     ys[i] = xy.y;
     s[i] = c.S.sscore[mem[i]];
@@ -301,7 +317,6 @@ struct FLevel<K, K, FILL> {
 #pragma unroll
       for (int i = 0; i < K; ++i) {
         c.S.flags[mem[i]] = 3;
-        c.S.smark[c.S.pos[mem[i]]] = 1;
       }
     }
   }
@@ -314,11 +329,11 @@ struct Stencil {
   double2 a;
 };
 
-template <int K>
+template <int K, bool W>
 __device__ __forceinline__ void stencil_setup(Stencil& st, int ts, const FShared& S,
                                               const FusedHdr& H) {
   const int key = S.scell[ts];
-  st.a = S.sxy[ts];
+  st.a = ld_xy<W>(S, ts);
   st.p = K;
   st.cx = 0;
   st.y0 = 0;
@@ -382,7 +397,7 @@ __device__ __forceinline__ bool edge_test(double2 a, double2 b, double B, double
 // P2 count for the box at sorted position ts (thread per box): JI test against every stencil
 // candidate of a higher picker; returns the edge count and the bitmask of edge candidates
 // (candidates 0..31 in stencil order; later candidates are re-tested by the fill).
-template <int K>
+template <int K, bool W>
 __device__ __forceinline__ int pairs_count(const Stencil& st, const FShared& S, const FusedHdr& H,
                                            double B, double two_b2, double i_lo, double i_hi,
                                            uint32_t* mask_out) {
@@ -394,7 +409,7 @@ __device__ __forceinline__ int pairs_count(const Stencil& st, const FShared& S, 
       int lo, hi;
       stencil_range(st, S, H, q, d, lo, hi);
       for (int t = lo; t < hi; ++t, ++kk) {
-        if (edge_test(st.a, S.sxy[t], B, two_b2, i_lo, i_hi)) {
+        if (edge_test(st.a, ld_xy<W>(S, t), B, two_b2, i_lo, i_hi)) {
           ++cnt;
           mask |= (kk < 32) ? (1u << kk) : 0u;
         }
@@ -407,7 +422,7 @@ __device__ __forceinline__ int pairs_count(const Stencil& st, const FShared& S, 
 
 // P2 fill: write the box's forward targets at d[0..cnt) from the count's bitmask (re-testing
 // candidates past the 32nd), then sort them by target (insertion sort; lists are short).
-template <int K>
+template <int K, bool W>
 __device__ __forceinline__ void pairs_fill(const Stencil& st, const FShared& S, const FusedHdr& H,
                                            uint32_t mask, uint16_t* d, int cnt, double B,
                                            double two_b2, double i_lo, double i_hi) {
@@ -430,7 +445,7 @@ __device__ __forceinline__ void pairs_fill(const Stencil& st, const FShared& S, 
         for (int t = lo; t < hi; ++t) {
           const int idx = kk + (t - lo);
           const bool e = idx < 32 ? ((mask >> idx) & 1u) != 0
-                                  : edge_test(st.a, S.sxy[t], B, two_b2, i_lo, i_hi);
+                                  : edge_test(st.a, ld_xy<W>(S, t), B, two_b2, i_lo, i_hi);
           if (e) d[c++] = S.citems[t];
         }
       }
@@ -445,23 +460,28 @@ __device__ __forceinline__ void pairs_fill(const Stencil& st, const FShared& S, 
   }
 }
 
-template <int K>
-__global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
+// Waves per SIMD the register allocator targets.  K = 3 fits 64 VGPRs (4 small spills) for 8
+// waves per SIMD = 4 workgroups per CU, which the f32-coordinate LDS layout also allows; larger
+// K keep the compiler's choice (their VGPRs, not LDS, bound the occupancy).
+constexpr int fused_waves_per_eu(int k) { return k <= 3 ? 8 : 1; }
+
+template <int K, bool W>
+__global__ __launch_bounds__(FWG) __attribute__((amdgpu_waves_per_eu(fused_waves_per_eu(K))))
+void k_fused(FusedArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   FusedHdr& H = *reinterpret_cast<FusedHdr*>(smem);
-  const FusedLayout L = fused_layout(A.nmax, A.ecap);
+  const FusedLayout L = fused_layout(A.nmax, A.ecap, W);
   FShared S;
-  S.sxy = reinterpret_cast<double2*>(smem + L.off_sxy);
+  S.sxy = smem + L.off_sxy;
   S.cstart = reinterpret_cast<uint16_t*>(smem + L.off_cstart);
   S.cnt = reinterpret_cast<uint32_t*>(smem + L.off_cnt);
-  S.fwd = reinterpret_cast<uint32_t*>(smem + L.off_fwd);
+  S.fwd = reinterpret_cast<uint16_t*>(smem + L.off_fwd);
   S.parent = reinterpret_cast<uint32_t*>(smem + L.off_parent);
   S.citems = reinterpret_cast<uint16_t*>(smem + L.off_citems);
   S.pos = reinterpret_cast<uint16_t*>(smem + L.off_pos);
   S.scell = reinterpret_cast<uint16_t*>(smem + L.off_scell);
   S.vrank = reinterpret_cast<uint16_t*>(smem + L.off_vrank);
   S.flags = reinterpret_cast<uint8_t*>(smem + L.off_flags);
-  S.smark = reinterpret_cast<uint8_t*>(smem + L.off_smark);
   S.dst = reinterpret_cast<uint16_t*>(smem + L.off_dst);
   S.sscore = reinterpret_cast<double*>(smem + L.off_parent);
   S.cbuf = reinterpret_cast<uint16_t*>(smem + L.off_cbuf);
@@ -528,12 +548,15 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
     for (int i = tid + RB * FWG; i < n; i += FWG) fn(i, A.x[b0 + i], A.y[b0 + i]);
   };
   double mnx = INFINITY, mny = INFINITY, mxx = -INFINITY, mxy = -INFINITY;
+  bool inexact = false;   // a coordinate not exactly representable as f32 (NaN excepted)
   each_box([&](int, double xv, double yv) {
     if (isfinite(xv) && isfinite(yv)) {
       mnx = fmin(mnx, xv); mxx = fmax(mxx, xv);
       mny = fmin(mny, yv); mxy = fmax(mxy, yv);
     }
+    if (!W) inexact |= ((double)(float)xv != xv && xv == xv) || ((double)(float)yv != yv && yv == yv);
   });
+  if (inexact) mnx = -INFINITY;   // (impossible otherwise) carried through the min reduction
   {
     double v[4] = {mnx, mny, -mxx, -mxy};
 #pragma unroll
@@ -551,6 +574,15 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
       for (int w = 1; w < FNW; ++w) v[r] = fmin(v[r], H.red4[r][w]);
     }
     mnx = v[0]; mny = v[1]; mxx = -v[2]; mxy = -v[3];
+  }
+  if (!W && mnx == -INFINITY) {   // needs the f64 layout: the host relaunches it wide
+    if (tid == 0) {
+      MgStat st = {};
+      st.status = RGC_ST_DEFER_WIDE;
+      st.target = -1;
+      A.st[m] = st;
+    }
+    return;
   }
 
   STOP_AFTER(0);
@@ -598,7 +630,6 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
   for (int i = tid; i < n; i += FWG) {
     S.parent[i] = i;
     S.flags[i] = 0;
-    S.smark[i] = 0;
   }
   for (int q = tid; q < (n + 1) / 2; q += FWG) ccsz[q] = 0;
   __syncthreads();
@@ -615,7 +646,7 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
     S.citems[t] = (uint16_t)i;
     S.pos[i] = (uint16_t)t;
     S.scell[t] = (uint16_t)q;
-    S.sxy[t] = make_double2(xv, yv);
+    st_xy<W>(S, t, xv, yv);
   });
   __syncthreads();
   // the cursors now hold key ends: rebuild the starts from the sorted keys
@@ -647,17 +678,17 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
   // each box's edge bitmask for the fill.
   for (int ts = tid; ts < n; ts += FWG) {
     Stencil st;
-    stencil_setup<K>(st, ts, S, H);
+    stencil_setup<K, W>(st, ts, S, H);
     uint32_t mask;
-    S.fwd[S.citems[ts]] = (uint32_t)pairs_count<K>(st, S, H, B, two_b2, i_lo, i_hi, &mask);
+    S.fwd[S.citems[ts]] = (uint16_t)pairs_count<K, W>(st, S, H, B, two_b2, i_lo, i_hi, &mask);
     S.cnt[ts] = mask;
   }
   __syncthreads();
   STAMP(3);   // count
   
-  const int64_t E = block_scan_array<FWG>(S.fwd, n, H.red64);
+  const int64_t E = block_scan_u16<FWG>(S.fwd, n, H.red64);
   if (tid == 0) {
-    S.fwd[n] = (uint32_t)E;
+    S.fwd[n] = (uint16_t)E;
     H.E = (int)E;
     if (E == 0) H.status = RGC_ST_NO_EDGES;
     else if (E > A.ecap) H.status = RGC_ST_DEFER;
@@ -671,9 +702,9 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
       const int base = S.fwd[i], cnt = (int)S.fwd[i + 1] - base;
       if (cnt == 0) continue;
       Stencil st;
-      stencil_setup<K>(st, ts, S, H);
+      stencil_setup<K, W>(st, ts, S, H);
       uint16_t* d = S.dst + base;
-      pairs_fill<K>(st, S, H, S.cnt[ts], d, cnt, B, two_b2, i_lo, i_hi);
+      pairs_fill<K, W>(st, S, H, S.cnt[ts], d, cnt, B, two_b2, i_lo, i_hi);
       S.flags[i] = 1;
       for (int e = 0; e < cnt; ++e) {
         const uint32_t h = d[e];
@@ -811,27 +842,29 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
     for (int q = tid; q <= n; q += FWG) bcnt[q] = 0;
     __syncthreads();
     for (int t = tid; t < n; t += FWG) {
-      if (!S.smark[t]) continue;
-      S.vrank[S.citems[t]] = (uint16_t)atomicAdd(&bcnt[xbucket(S.sxy[t].x)], 1u);
+      const int vi = S.citems[t];
+      if (S.flags[vi] != 3) continue;
+      S.vrank[vi] = (uint16_t)atomicAdd(&bcnt[xbucket(ld_xy<W>(S, t).x)], 1u);
     }
     __syncthreads();
     const int64_t V = block_scan_array<FWG>(bcnt, n, H.red64);
     if (tid == 0) { H.V = (int)V; bcnt[n] = (uint32_t)V; }
     for (int t = tid; t < n; t += FWG) {
-      if (!S.smark[t]) continue;
-      blist[bcnt[xbucket(S.sxy[t].x)] + S.vrank[S.citems[t]]] = (uint16_t)t;
+      const int vi = S.citems[t];
+      if (S.flags[vi] != 3) continue;
+      blist[bcnt[xbucket(ld_xy<W>(S, t).x)] + S.vrank[vi]] = (uint16_t)t;
     }
     __syncthreads();
     for (int t = tid; t < n; t += FWG) {
-      if (!S.smark[t]) continue;
-      const double2 v = S.sxy[t];
       const int vi = S.citems[t];
+      if (S.flags[vi] != 3) continue;
+      const double2 v = ld_xy<W>(S, t);
       const int b = xbucket(v.x);
       const int lo = bcnt[b], hi = bcnt[b + 1];
       uint32_t rk = lo;
       for (int u = lo; u < hi; ++u) {
         const int tu = blist[u];
-        const double2 w = S.sxy[tu];
+        const double2 w = ld_xy<W>(S, tu);
         const int ui = S.citems[tu];
         rk += (w.x < v.x) || (w.x == v.x && (w.y < v.y || (w.y == v.y && ui < vi)));
       }
@@ -857,7 +890,7 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
         const uint16_t* sb = S.cbuf + sl * K;
 #pragma unroll
         for (int i = 0; i < K; ++i) mem[i] = sb[i];
-        fused_epilogue<K>(c, H.base + S.cnt[mem[0]] + c.cq_ord[sl], mem);
+        fused_epilogue<K, W>(c, H.base + S.cnt[mem[0]] + c.cq_ord[sl], mem);
       }
     } else {
       for (int64_t c0 = 0; c0 < Cm; c0 += cbuf_cap) {
@@ -878,7 +911,7 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
           const uint16_t* sb = S.cbuf + (j - c0) * K;
 #pragma unroll
           for (int i = 0; i < K; ++i) mem[i] = sb[i];
-          fused_epilogue<K>(c, H.base + j, mem);
+          fused_epilogue<K, W>(c, H.base + j, mem);
         }
         __syncthreads();
       }
@@ -900,22 +933,46 @@ __global__ __launch_bounds__(FWG) void k_fused(FusedArgs A) {
   }
 }
 
-int launch_fused(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArgs& A) {
+template <int K, bool W>
+static int launch_fused_t(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArgs& A) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused<K, W>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+      return -2;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((k_fused<K, W>), dim3(n_blocks), dim3(FWG), lds_bytes, stream, A);
+  return 0;
+}
+
+template <int K, bool W>
+static int fused_vgprs_t() {
+  hipFuncAttributes at;
+  if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&k_fused<K, W>)) != hipSuccess)
+    return -1;
+  return at.numRegs;
+}
+
+int fused_vgprs(int k, bool wide) {
+  switch (k) {
+#define RGC_VG_CASE(KK) \
+  case KK: return wide ? fused_vgprs_t<KK, true>() : fused_vgprs_t<KK, false>();
+    RGC_VG_CASE(2) RGC_VG_CASE(3) RGC_VG_CASE(4) RGC_VG_CASE(5) RGC_VG_CASE(6) RGC_VG_CASE(7)
+    RGC_VG_CASE(8)
+#undef RGC_VG_CASE
+    default:
+      return -1;
+  }
+}
+
+int launch_fused(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArgs& A, bool wide) {
   if (n_blocks <= 0) return 0;
   switch (A.k) {
-#define RGC_FUSED_CASE(KK)                                                                    \
-  case KK: {                                                                                  \
-    static bool attr_set = false;                                                             \
-    if (!attr_set) {                                                                          \
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused<KK>),                    \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=     \
-          hipSuccess)                                                                         \
-        return -2;                                                                            \
-      attr_set = true;                                                                        \
-    }                                                                                         \
-    hipLaunchKernelGGL(k_fused<KK>, dim3(n_blocks), dim3(FWG), lds_bytes, stream, A);          \
-    break;                                                                                    \
-  }
+#define RGC_FUSED_CASE(KK)                                                          \
+  case KK:                                                                          \
+    return wide ? launch_fused_t<KK, true>(stream, n_blocks, lds_bytes, A)          \
+                : launch_fused_t<KK, false>(stream, n_blocks, lds_bytes, A);
     RGC_FUSED_CASE(2)
     RGC_FUSED_CASE(3)
     RGC_FUSED_CASE(4)

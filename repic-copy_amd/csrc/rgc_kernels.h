@@ -28,6 +28,7 @@ constexpr int RGC_ST_NO_EDGES = 1;
 constexpr int RGC_ST_NO_CLIQUES = 2;
 constexpr int RGC_ST_DEFER = 3;      // does not fit the fused kernel's LDS capacities
 constexpr int RGC_ST_OVERFLOW = 4;   // output capacity exceeded: host grows and re-runs
+constexpr int RGC_ST_DEFER_WIDE = 5; // coordinates not exact in f32: rerun with the f64 layout
 
 // LDS layout of the fused kernel for a size class (byte offsets into dynamic LDS)
 struct FusedLayout {
@@ -57,8 +58,9 @@ struct FusedArgs {
   unsigned long long* stamps;   // diagnostic build (RGC_STAMPS) only: 8 stamps per WG
 };
 
-int fused_lds_bytes(int nmax, int ecap);
-int launch_fused(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArgs& A);
+int fused_lds_bytes(int nmax, int ecap, bool wide);
+int fused_vgprs(int k, bool wide);
+int launch_fused(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArgs& A, bool wide);
 void launch_gather(hipStream_t stream, int n_sub, int k, const int32_t* sub_mg,
                    const int32_t* box_off, const int32_t* sub_box_off, const double* x,
                    const double* y, const double* s, double* ox, double* oy, double* os,
