@@ -81,7 +81,7 @@ static int lds_blocks(int bytes) { return (bytes + LDS_BLOCK - 1) / LDS_BLOCK; }
 // One fused launch configuration: micrographs of <= nmax boxes, forward-edge capacity ecap,
 // dynamic LDS bytes, coordinate width.
 struct FusedPlan {
-  int nmax = 0, ecap = 0, lds = 0;
+  int nmax = 0, ecap = 0, lds = 0, wg = 0;   // wg: workgroups per CU
   bool wide = false;
 };
 
@@ -111,6 +111,7 @@ static bool plan_fused(int k, bool wide, int nmax, int max_wg, FusedPlan* p) {
   p->nmax = nmax;
   p->ecap = ecap;
   p->wide = wide;
+  p->wg = w;
   p->lds = fused_lds_bytes(nmax, ecap, wide);
   return p->lds <= budget;
 }
@@ -525,24 +526,40 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
         }
         std::vector<int32_t> by;
         std::vector<size_t> starts;
-        for (size_t q = 0; q < keys.size(); ++q) {
-          starts.push_back(by.size());
-          by.insert(by.end(), lists[q].begin(), lists[q].end());
+        // every micrograph in one launch (identity list) when the largest class runs at the
+        // occupancy of every smaller one: no list upload, no tail per class
+        bool single = pass == 0 && (int)todo.size() == n_mg && left.empty() && !keys.empty();
+        if (single) {
+          int cmax = 0;
+          for (int cl : keys) cmax = std::max(cmax, cl);
+          for (int cl : keys) single = single && plan_of(0, cl).wg == plan_of(0, cmax).wg;
+          if (single) {
+            keys.assign(1, cmax);
+            lists.assign(1, std::vector<int32_t>());
+            by = todo;
+            starts.push_back(0);
+          }
         }
-        std::memcpy(f_ml + ml_off, by.data(), by.size() * 4);
-        if (!by.empty())
-          HIPCHK(hipMemcpyAsync(D<int32_t>(c, D_MGLIST) + ml_off, f_ml + ml_off, by.size() * 4,
-                                hipMemcpyHostToDevice, s));
+        if (!single) {
+          for (size_t q = 0; q < keys.size(); ++q) {
+            starts.push_back(by.size());
+            by.insert(by.end(), lists[q].begin(), lists[q].end());
+          }
+          std::memcpy(f_ml + ml_off, by.data(), by.size() * 4);
+          if (!by.empty())
+            HIPCHK(hipMemcpyAsync(D<int32_t>(c, D_MGLIST) + ml_off, f_ml + ml_off, by.size() * 4,
+                                  hipMemcpyHostToDevice, s));
+        }
         for (size_t q = 0; q < keys.size(); ++q) {
           const FusedPlan& pl = plan_of(pass, keys[q]);
           A.nmax = pl.nmax;
           A.ecap = pl.ecap;
-          A.mg_list = D<int32_t>(c, D_MGLIST) + ml_off + starts[q];
+          A.mg_list = single ? nullptr : D<int32_t>(c, D_MGLIST) + ml_off + starts[q];
 #ifdef RGC_STAMPS
           A.stamps = D<unsigned long long>(c, D_STAMPS) + (size_t)(ml_off + starts[q]) * 16;
 #endif
           TRY(mark(c, "k_fused"));
-          if (launch_fused(s, (int)lists[q].size(), pl.lds, A, wide) != 0)
+          if (launch_fused(s, single ? n_mg : (int)lists[q].size(), pl.lds, A, wide) != 0)
             return fail("fused kernel launch failed");
         }
         TRY(mark(c, "d2h_stats"));

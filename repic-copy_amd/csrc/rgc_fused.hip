@@ -488,7 +488,7 @@ void k_fused(FusedArgs A) {
   const int cbuf_bytes = L.off_parent - L.off_cbuf;
   const int cbuf_cap = cbuf_bytes / (2 * K);         // cliques per P6 re-walk chunk
   const int tid = threadIdx.x;
-  const int m = A.mg_list[blockIdx.x];
+  const int m = A.mg_list ? A.mg_list[blockIdx.x] : (int)blockIdx.x;
 #ifdef RGC_STAMPS
   // diagnostic build only: per-phase s_memtime stamps of thread 0 (never in the product .so)
 #define STAMP(i)                                                                            \

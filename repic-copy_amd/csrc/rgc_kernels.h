@@ -40,7 +40,7 @@ struct FusedArgs {
   int k, flags;                 // flags: bit0 get_cc, bit1 multi_out, bit5 members
   double B, two_b2;
   int nmax, ecap;               // LDS capacities of this launch (boxes, forward edges)
-  const int32_t* mg_list;       // micrographs of this size class
+  const int32_t* mg_list;       // micrographs of this launch (nullptr: block b = micrograph b)
   const int32_t* box_off;
   const int64_t* id_base;
   const double* x;

@@ -218,17 +218,22 @@ class Result:
         self.n_mg, self.k = n_mg, k
         self.n_boxes, self.n_edges, self.n_cliques = bo.n_boxes, bo.n_edges, bo.n_cliques
 
-        def a(p, n):
-            return np.ctypeslib.as_array(p, shape=(n,)).copy() if n else np.zeros(0)
+        def a(p, n, dt):
+            """copy of n library-owned values (the library reuses the memory next run)"""
+            dt = np.dtype(dt)
+            if not n:
+                return np.zeros(0, dt)
+            addr = C.cast(p, C.c_void_p).value
+            return np.frombuffer((C.c_char * (n * dt.itemsize)).from_address(addr), dt).copy()
 
-        self.status = a(bo.status, n_mg).astype(np.int32)
-        self.cc_max = a(bo.cc_max, n_mg).astype(np.int32)
-        self.cc_cnt = a(bo.cc_cnt, n_mg).astype(np.int32)
-        self.n_nodes = a(bo.n_nodes, n_mg).astype(np.int32)
-        self.n_vert = a(bo.n_vert, n_mg).astype(np.int32)
-        self.n_edges_mg = a(bo.n_edges_mg, n_mg).astype(np.int64)
-        self.clique_base = a(bo.clique_base, n_mg).astype(np.int64)
-        self.clique_cnt = a(bo.clique_cnt, n_mg).astype(np.int64)
+        self.status = a(bo.status, n_mg, np.int32)
+        self.cc_max = a(bo.cc_max, n_mg, np.int32)
+        self.cc_cnt = a(bo.cc_cnt, n_mg, np.int32)
+        self.n_nodes = a(bo.n_nodes, n_mg, np.int32)
+        self.n_vert = a(bo.n_vert, n_mg, np.int32)
+        self.n_edges_mg = a(bo.n_edges_mg, n_mg, np.int64)
+        self.clique_base = a(bo.clique_base, n_mg, np.int64)
+        self.clique_cnt = a(bo.clique_cnt, n_mg, np.int64)
         C_ = int(self.n_cliques)
         if flags & F_HOST_OUTPUTS:
             def h(p, ct, n):
