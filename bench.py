@@ -32,13 +32,19 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 DEFAULT_MG = {"C2": 10000, "C3": 1000, "C4": 12500, "C5": 8}
 
 
+def fused_compulsory_bytes(N, C, k, V, n_mg):
+    """Bytes the fused kernel must move at minimum: read x, y (16 B/box) and the scores of
+    clique vertices (8 B/vertex); write rows (4k), w, conf, consensus (12) per clique and the
+    48-B per-micrograph stats."""
+    return 16 * N + 8 * V + C * (4 * k + 12) + 48 * n_mg
+
+
 def alg_bytes(name, N, E, C, k, V, n_mg=0):
-    """Algorithmic (compulsory) HBM bytes of one launch of each kernel."""
+    """Algorithmic HBM bytes of one step of each kernel.  The fused kernel
+    runs the whole hot path, so its figure is SURVEY.md §8(d)'s per-micrograph B_alg summed
+    over the micrographs it processes."""
     table = {
-        # fused per-micrograph kernel: read x, y (16 B/box) and the scores of clique vertices
-        # (8 B/vertex); write rows (4k), w, conf, consensus (12) per clique and 56 B of
-        # per-micrograph stats
-        "k_fused": 16 * N + 8 * V + C * (4 * k + 12) + 56 * n_mg,
+        "k_fused": pipeline_bytes(N, E, C, k),
         "k1_bin": 16 * N + 30 * N,                       # read x,y; write sorted SoA + maps
         "k2_pairs_count": 21 * N + 4 * N,                # read sx,sy,spick,sbox; write count
         "k2_pairs_fill": 21 * N + 8 * N + 12 * E,        # + offsets; write (dst, JI) per edge
@@ -204,8 +210,10 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": traffic_src,
-                     "alg_bytes_per_launch": dom_bytes,
-                     "avg_launch_ms": avg[dom]},
+                     "alg_bytes_per_step": dom_bytes, "alg_bytes_formula":
+                         "SURVEY.md 8(d): 28 N + 32 E + C (20 k + 12)",
+                     "compulsory_bytes_per_step": fused_compulsory_bytes(N, C, cfg.k, V, n_mg),
+                     "kernel_ms_per_step": avg[dom]},
         "pipeline": {"device_ms_per_step": dev_ms, "alg_bytes": pipe,
                      "achieved_gbs": pipe / (dev_ms * 1e-3) / 1e9,
                      "frac": pipe / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
