@@ -90,6 +90,7 @@ struct FShared {
   uint16_t* vrank;
   uint8_t* flags;   // by local index: 0 no edge, 1 graph node, 3 clique vertex
   uint16_t* dst;
+  uint16_t* split;  // P3-P4 (scell region): end of each box's first picker segment in dst
   double* sscore;   // P6 only (parent..scell): scores of clique vertices by local index
   uint16_t* cbuf;   // P4-P6 (cell starts): clique queue, or the current chunk of the re-walk
 };
@@ -166,6 +167,15 @@ __device__ __forceinline__ int picker_end(const int (&pb)[K + 1], int i) {
   int e = pb[1];
 #pragma unroll
   for (int q = 1; q < K; ++q) e += (i >= pb[q]) ? (pb[q + 1] - pb[q]) : 0;
+  return e;
+}
+// end (in box index) of the picker after box i's picker: targets of box i below it form the
+// first segment of i's forward list
+template <int K>
+__device__ __forceinline__ int next_picker_end(const int (&pb)[K + 1], int i) {
+  int e = pb[K < 2 ? K : 2];
+#pragma unroll
+  for (int q = 1; q < K; ++q) e += (i >= pb[q]) ? (q + 2 <= K ? pb[q + 2] - pb[q + 1] : 0) : 0;
   return e;
 }
 template <int K>
@@ -277,10 +287,14 @@ __device__ __forceinline__ void fused_epilogue(const FCtx<K>& c, int64_t j, cons
 template <int K, int D, bool FILL>
 struct FLevel {
   __device__ __forceinline__ static void run(FCtx<K>& c, int (&mem)[K]) {
+    // the picker-D neighbours of mem[D-1] (a picker D-1 box) are the first segment of its
+    // forward list: [fwd, split) from P3, or by binary search in the P6 re-walk (split's
+    // LDS is reused by then)
     const int prev = mem[D - 1];
-    const int l0 = c.S.fwd[prev], h0 = c.S.fwd[prev + 1];
-    const int lo = lb16(c.S.dst, l0, h0, c.pb[D]);
-    const int hi = lb16(c.S.dst, lo, h0, c.pb[D + 1]);
+    const int lo = c.S.fwd[prev];
+    int hi;
+    if (FILL) hi = lb16(c.S.dst, lo, c.S.fwd[prev + 1], c.pb[D + 1]);
+    else hi = c.S.split[prev];
     for (int e = lo; e < hi; ++e) {
       const int h = c.S.dst[e];
       bool ok = true;
@@ -476,6 +490,7 @@ void k_fused(FusedArgs A) {
   S.cstart = reinterpret_cast<uint16_t*>(smem + L.off_cstart);
   S.cnt = reinterpret_cast<uint32_t*>(smem + L.off_cnt);
   S.fwd = reinterpret_cast<uint16_t*>(smem + L.off_fwd);
+  S.split = reinterpret_cast<uint16_t*>(smem + L.off_scell);
   S.parent = reinterpret_cast<uint32_t*>(smem + L.off_parent);
   S.citems = reinterpret_cast<uint16_t*>(smem + L.off_citems);
   S.pos = reinterpret_cast<uint16_t*>(smem + L.off_pos);
@@ -633,32 +648,26 @@ void k_fused(FusedArgs A) {
   }
   for (int q = tid; q < (n + 1) / 2; q += FWG) ccsz[q] = 0;
   __syncthreads();
+  // counts go to slot key + 1, so the exclusive scan leaves bucket q's start in slot q + 1;
+  // the scatter's cursors advance it to bucket q's end = bucket q+1's start, which leaves
+  // cstart[q] = start of bucket q for q = 0..nk+1 with no rebuild pass.  The key waits in
+  // pos[i] between the two passes.
   each_box([&](int i, double xv, double yv) {
-    const int q = box_key(H, picker_of<K>(c.pb, i), xv, yv);
+    const int q = box_key(H, picker_of<K>(c.pb, i), xv, yv) + 1;
+    S.pos[i] = (uint16_t)q;
     atomicAdd(&cw[q >> 1], 1u << (16 * (q & 1)));
   });
   __syncthreads();
-  block_scan_u16<FWG>(S.cstart, nk + 1, H.red64);
+  block_scan_u16<FWG>(S.cstart, nk + 2, H.red64);
   each_box([&](int i, double xv, double yv) {
-    const int q = box_key(H, picker_of<K>(c.pb, i), xv, yv);
+    const int q = S.pos[i];
     const int sh = 16 * (q & 1);
     const int t = (atomicAdd(&cw[q >> 1], 1u << sh) >> sh) & 0xFFFF;
     S.citems[t] = (uint16_t)i;
     S.pos[i] = (uint16_t)t;
-    S.scell[t] = (uint16_t)q;
+    S.scell[t] = (uint16_t)(q - 1);
     st_xy<W>(S, t, xv, yv);
   });
-  __syncthreads();
-  // the cursors now hold key ends: rebuild the starts from the sorted keys
-  for (int t = tid; t < n; t += FWG) {
-    const int q = S.scell[t];
-    const int qp = t ? (int)S.scell[t - 1] : -1;
-    for (int qq = qp + 1; qq <= q; ++qq) S.cstart[qq] = (uint16_t)t;
-    if (t == n - 1)
-      for (int qq = q + 1; qq <= nk + 1; ++qq) S.cstart[qq] = (uint16_t)n;
-  }
-  if (n == 0 && tid == 0)
-    for (int qq = 0; qq <= nk + 1; ++qq) S.cstart[qq] = 0;
   __syncthreads();
 
   STOP_AFTER(1);
@@ -739,6 +748,8 @@ void k_fused(FusedArgs A) {
   STAMP(6);   // (empty: union fused into the fill)
   for (int i = tid; i < n; i += FWG) {
     if (!S.flags[i]) continue;
+    const int e0 = S.fwd[i], e1 = S.fwd[i + 1];
+    S.split[i] = (uint16_t)lb16(S.dst, e0, e1, next_picker_end<K>(c.pb, i));   // every node
     const uint32_t r = uf_find_lds(S.parent, i);
     lds_st(S.parent + i, r);
     atomicAdd(&ccsz[r >> 1], 1u << (16 * (r & 1)));
