@@ -559,8 +559,12 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
           A.stamps = D<unsigned long long>(c, D_STAMPS) + (size_t)(ml_off + starts[q]) * 16;
 #endif
           TRY(mark(c, "k_fused"));
-          if (launch_fused(s, single ? n_mg : (int)lists[q].size(), pl.lds, A, wide) != 0)
-            return fail("fused kernel launch failed");
+          const int le = launch_fused(s, single ? n_mg : (int)lists[q].size(), pl.lds, A, wide);
+          if (le != 0)
+            return fail(std::string("fused kernel launch failed (k=") + std::to_string(k) +
+                        (wide ? ", f64" : ", f32") + " layout, nmax " + std::to_string(pl.nmax) +
+                        ", lds " + std::to_string(pl.lds) + "): " +
+                        (le > 0 ? hipGetErrorString((hipError_t)le) : "unsupported k"));
         }
         TRY(mark(c, "d2h_stats"));
         HIPCHK(hipMemcpyAsync(H<void>(c, H_FSTAT), D<void>(c, D_FSTAT), n_mg * sizeof(MgStat),

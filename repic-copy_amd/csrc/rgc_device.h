@@ -176,21 +176,73 @@ struct Epi {
   int8_t ord[K];  // networkx node-iteration order (picker indices)
 };
 
-// mem[i]  : any box handle, only used to break (x, y) ties by id order (monotone in handle)
-// ji[i][j]: JI of members i < j;  s[i]: scores;  xs/ys: coordinates;  ids: global box ids
-// set_order: networkx iterates set(sorted(clique)) (2k < |G|) vs graph insertion order;
-// ins[i]  : graph insertion key of member i (used only when !set_order)
-// All private arrays are indexed with compile-time indices only (no scratch).
+// networkx node-iteration order of a clique (nibble r = member index of the r-th node): set
+// order = CPython set(sorted(clique)) iteration (2k < |G|), else graph insertion order.
+// Needed only on weighted-degree ties or for --multi_out.
 template <int K>
-__host__ __device__ __forceinline__ void epilogue(const int (&mem)[K], const double (&ji)[K][K],
-                                         const double (&s)[K], const double (&xs)[K],
-                                         const double (&ys)[K], const int64_t (&ids)[K],
-                                         bool set_order, const uint64_t (&ins)[K], bool need_order,
-                                         Epi<K>& out) {
+__host__ __device__ __forceinline__ uint32_t node_order(const int (&mem)[K], const double (&xs)[K],
+                                                     const double (&ys)[K],
+                                                     const int64_t (&ids)[K], bool set_order,
+                                                     const uint64_t (&ins)[K]) {
+  // Sorting is done by ranks (rank_i = number of members ordered before member i), so no
+  // private array is ever permuted or dynamically indexed.
+  uint32_t inv = 0;   // nibble t = member index at sorted position t
+  uint32_t ord = 0;
+  if (set_order) {
+    // insertion order = sorted (x, y, id); then CPython set iteration order
+    uint64_t hs[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      int rk = 0;
+#pragma unroll
+      for (int q = 0; q < K; ++q) {
+        const bool lt = (xs[q] < xs[i]) ||
+                        (xs[q] == xs[i] && (ys[q] < ys[i] || (ys[q] == ys[i] && mem[q] < mem[i])));
+        rk += lt ? 1 : 0;
+      }
+      inv |= (uint32_t)i << (4 * rk);
+    }
+    // hashes in insertion (sorted) order: hs[t] = hash of the member at position t
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      const int i = (inv >> (4 * t)) & 15;
+      double hx = xs[0], hy = ys[0];
+      int64_t hid = ids[0];
+#pragma unroll
+      for (int q = 1; q < K; ++q) {
+        const bool h = (i == q);
+        hx = h ? xs[q] : hx;
+        hy = h ? ys[q] : hy;
+        hid = h ? ids[q] : hid;
+      }
+      hs[t] = pyset::hash_node(hx, hy, hid);
+    }
+    const uint32_t so = pyset::set_order_packed<K>(hs);
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+      const int t = (so >> (4 * r)) & 15;
+      ord |= ((inv >> (4 * t)) & 15) << (4 * r);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      int rk = 0;
+#pragma unroll
+      for (int q = 0; q < K; ++q) rk += (ins[q] < ins[i] || (ins[q] == ins[i] && q < i)) ? 1 : 0;
+      ord |= (uint32_t)i << (4 * rk);
+    }
+  }
+  return ord;
+}
+
+// conf = f32(median(scores)), w = f32(f64(conf) * median(JIs)) (get_cliques.py:169-170,186-190)
+template <int K>
+__host__ __device__ __forceinline__ void epi_weights(const double (&ji)[K][K], const double (&s)[K],
+                                                     float* w, float* conf) {
   double sc[K];
 #pragma unroll
   for (int i = 0; i < K; ++i) sc[i] = s[i];
-  const double conf = median_n<K>(sc);
+  const double cf = median_n<K>(sc);
   constexpr int NE = K * (K - 1) / 2;
   double ej[NE];
   {
@@ -201,11 +253,16 @@ __host__ __device__ __forceinline__ void epilogue(const int (&mem)[K], const dou
       for (int b = a + 1; b < K; ++b) ej[t++] = ji[a][b];
   }
   const double med = median_n<NE>(ej);
-  const float conf32 = (float)conf;
-  out.conf = conf32;
-  out.w = (float)((double)conf32 * med);
-  // weighted degree: JIs to the other members summed in increasing picker order
-  // (networkx DegreeView over adjacency insertion order; naive left-to-right f64 sum)
+  const float conf32 = (float)cf;
+  *conf = conf32;
+  *w = (float)((double)conf32 * med);
+}
+
+// weighted degrees: JIs to the other members summed in increasing picker order (networkx
+// DegreeView over adjacency insertion order; naive left-to-right f64 sum, :182-183); returns
+// the first maximal member and the bitmask of all maximal members
+template <int K>
+__host__ __device__ __forceinline__ int epi_degree_max(const double (&ji)[K][K], uint32_t* top) {
   double deg[K];
 #pragma unroll
   for (int i = 0; i < K; ++i) {
@@ -218,73 +275,48 @@ __host__ __device__ __forceinline__ void epilogue(const int (&mem)[K], const dou
     deg[i] = d;
   }
   double dmax = deg[0];
-  int nmax = 1, arg = 0;
+  int arg = 0;
 #pragma unroll
-  for (int i = 1; i < K; ++i) {
-    if (deg[i] > dmax) { dmax = deg[i]; nmax = 1; arg = i; }
-    else if (deg[i] == dmax) ++nmax;
+  for (int i = 1; i < K; ++i)
+    if (deg[i] > dmax) { dmax = deg[i]; arg = i; }
+  uint32_t t = 0;
+#pragma unroll
+  for (int i = 0; i < K; ++i) t |= (deg[i] == dmax ? 1u : 0u) << i;
+  *top = t;
+  return arg;
+}
+
+// consensus among tied maximal members: the first of them in node-iteration order
+template <int K>
+__host__ __device__ __forceinline__ int epi_tie_arg(uint32_t top, uint32_t ord) {
+  int arg = 0;
+  bool found = false;
+#pragma unroll
+  for (int r = 0; r < K; ++r) {
+    const int mi = (ord >> (4 * r)) & 15;
+    if (!found && ((top >> mi) & 1u)) { arg = mi; found = true; }
   }
-  if (nmax > 1 || need_order) {
-    // ord: nibble r = member index of the r-th node in networkx node-iteration order.
-    // Sorting is done by ranks (rank_i = number of members ordered before member i), so no
-    // private array is ever permuted or dynamically indexed.
-    uint32_t inv = 0;   // nibble t = member index at sorted position t
-    uint32_t ord = 0;
-    if (set_order) {
-      // insertion order = sorted (x, y, id); then CPython set iteration order
-      uint64_t hs[K];
-#pragma unroll
-      for (int i = 0; i < K; ++i) {
-        int rk = 0;
-#pragma unroll
-        for (int q = 0; q < K; ++q) {
-          const bool lt = (xs[q] < xs[i]) ||
-                          (xs[q] == xs[i] && (ys[q] < ys[i] || (ys[q] == ys[i] && mem[q] < mem[i])));
-          rk += lt ? 1 : 0;
-        }
-        inv |= (uint32_t)i << (4 * rk);
-      }
-      // hashes in insertion (sorted) order: hs[t] = hash of the member at position t
-#pragma unroll
-      for (int t = 0; t < K; ++t) {
-        const int i = (inv >> (4 * t)) & 15;
-        double hx = xs[0], hy = ys[0];
-        int64_t hid = ids[0];
-#pragma unroll
-        for (int q = 1; q < K; ++q) {
-          const bool h = (i == q);
-          hx = h ? xs[q] : hx;
-          hy = h ? ys[q] : hy;
-          hid = h ? ids[q] : hid;
-        }
-        hs[t] = pyset::hash_node(hx, hy, hid);
-      }
-      const uint32_t so = pyset::set_order_packed<K>(hs);
-#pragma unroll
-      for (int r = 0; r < K; ++r) {
-        const int t = (so >> (4 * r)) & 15;
-        ord |= ((inv >> (4 * t)) & 15) << (4 * r);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < K; ++i) {
-        int rk = 0;
-#pragma unroll
-        for (int q = 0; q < K; ++q) rk += (ins[q] < ins[i] || (ins[q] == ins[i] && q < i)) ? 1 : 0;
-        ord |= (uint32_t)i << (4 * rk);
-      }
-    }
-    if (nmax > 1) {
-      uint32_t top = 0;   // members whose degree equals the maximum
-#pragma unroll
-      for (int i = 0; i < K; ++i) top |= (deg[i] == dmax ? 1u : 0u) << i;
-      bool found = false;
-#pragma unroll
-      for (int r = 0; r < K; ++r) {
-        const int mi = (ord >> (4 * r)) & 15;
-        if (!found && ((top >> mi) & 1u)) { arg = mi; found = true; }
-      }
-    }
+  return arg;
+}
+
+// mem[i]  : any box handle, only used to break (x, y) ties by id order (monotone in handle)
+// ji[i][j]: JI of members i < j;  s[i]: scores;  xs/ys: coordinates;  ids: global box ids
+// set_order: networkx iterates set(sorted(clique)) (2k < |G|) vs graph insertion order;
+// ins[i]  : graph insertion key of member i (used only when !set_order)
+// All private arrays are indexed with compile-time indices only (no scratch).
+template <int K>
+__host__ __device__ __forceinline__ void epilogue(const int (&mem)[K], const double (&ji)[K][K],
+                                         const double (&s)[K], const double (&xs)[K],
+                                         const double (&ys)[K], const int64_t (&ids)[K],
+                                         bool set_order, const uint64_t (&ins)[K], bool need_order,
+                                         Epi<K>& out) {
+  epi_weights<K>(ji, s, &out.w, &out.conf);
+  uint32_t top;
+  int arg = epi_degree_max<K>(ji, &top);
+  const bool tie = (top & (top - 1)) != 0;
+  if (tie || need_order) {
+    const uint32_t ord = node_order<K>(mem, xs, ys, ids, set_order, ins);
+    if (tie) arg = epi_tie_arg<K>(top, ord);
 #pragma unroll
     for (int i = 0; i < K; ++i) out.ord[i] = (int8_t)((ord >> (4 * i)) & 15);
   }

@@ -1,8 +1,11 @@
 // rgc_fused.hip — the whole get_cliques hot path for one micrograph in ONE workgroup.
 //
 // Everything between reading a micrograph's boxes and writing its ILP structures stays in
-// LDS: boxes (f64 x/y), the uniform grid (x-major cells, side >= box_size), the forward
-// adjacency CSR (u16 targets), union-find, the clique DFS and the vertex ranks.  HBM sees
+// LDS: boxes (f32 or f64 x/y), one uniform grid per picker, the forward adjacency CSR (u16
+// targets), union-find, the clique DFS and the vertex ranks.  Graph nodes are the boxes'
+// SORTED POSITIONS (picker-major grid order, local index order inside a cell): stencil
+// ranges then yield every forward list already sorted, and all per-node arrays are indexed
+// by position; local (file-order) indices only enter where the reference orders by box id.  HBM sees
 // the compulsory traffic only: 16 B/box of coordinates in, 8 B per clique member of scores
 // in (gathered), and C*(4k + 12) bytes of clique outputs out.  No global scans, no
 // mid-pipeline host syncs, no global atomics except one clique-range reservation per
@@ -46,6 +49,7 @@ struct FusedHdr {
   int gx, gy, ncell, nkey;   // per-picker grid gx x gy; keys picker * ncell + cell; nkey = none
   int E, nodes, cc_cnt, cc_max, target, V, status;
   uint32_t ccur;    // P4 clique-queue cursor
+  int tief[2];      // P6: some clique of the chunk needs the order pass (by chunk parity)
   int64_t C, base;
 };
 
@@ -67,8 +71,8 @@ __host__ __device__ inline FusedLayout fused_layout(int nmax, int ecap, bool wid
   L.off_union = o;
   L.off_cstart = o; o += al(2 * (4 * nmax + 8));   // u16 cell starts, <= 4n + 1 cells
   L.off_parent = o; o += al(4 * (nmax + 4));
-  L.off_citems = o; o += al(2 * nmax);        // sorted position -> local box index
   L.off_scell = o; o += al(2 * nmax);         // sorted position -> cell
+  L.off_citems = o; o += al(2 * nmax);        // sorted position -> local box index
   L.off_flags = o; o += al(nmax);             // by local index: 1 graph node, 3 clique vertex
   L.off_smark = o;
   L.total = o;
@@ -91,8 +95,11 @@ struct FShared {
   uint8_t* flags;   // by local index: 0 no edge, 1 graph node, 3 clique vertex
   uint16_t* dst;
   uint16_t* split;  // P3-P4 (scell region): end of each box's first picker segment in dst
-  double* sscore;   // P6 only (parent..scell): scores of clique vertices by local index
   uint16_t* cbuf;   // P4-P6 (cell starts): clique queue, or the current chunk of the re-walk
+  double* vscore;   // P6 (parent..scell, dead after P5): score of each clique vertex by row
+                    // rank, used when 8 V bytes fit there (vstaged); else scores are
+                    // gathered from HBM
+  bool vstaged;
 };
 
 template <bool W>
@@ -125,6 +132,7 @@ struct FCtx {
   uint8_t* order;
   FShared S;
   int pb[K + 1];     // picker bounds (local box indices)
+  int pp[K + 1];     // picker bounds (sorted positions; pp[K] = first non-finite box)
   int m, b0, n;
   int64_t idb;       // global id of local box 0
   bool set_order;    // networkx iterates set(sorted(clique)) (2k < |G|)
@@ -199,86 +207,166 @@ __device__ __forceinline__ bool contains16(const uint16_t* a, int lo, int hi, in
   return p < hi && (int)a[p] == v;
 }
 
+// wave-uniform copies (SGPRs) of values every lane reads from the LDS header
+__device__ __forceinline__ int ufl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float uff(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+__device__ __forceinline__ double ufd(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xFFFFFFFF));
+  const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// the micrograph's grid geometry, uniform across the workgroup
+struct GridU {
+  double minx, miny, inv_cell;
+  float inv_gy;
+  int gx, gy, ncell, nkey;
+};
+__device__ __forceinline__ GridU grid_u(const FusedHdr& H) {
+  GridU G;
+  G.minx = ufd(H.minx); G.miny = ufd(H.miny); G.inv_cell = ufd(H.inv_cell);
+  G.inv_gy = uff(H.inv_gy);
+  G.gx = ufl(H.gx); G.gy = ufl(H.gy); G.ncell = ufl(H.ncell); G.nkey = ufl(H.nkey);
+  return G;
+}
+
 // P1 sort key of a box of picker p: its cell in picker p's grid (x-major), or nkey when the
 // box cannot have an edge (non-finite coordinates).  Monotone in x and y per picker.
-__device__ __forceinline__ int box_key(const FusedHdr& H, int p, double x, double y) {
+__device__ __forceinline__ int box_key(const GridU& H, int p, double x, double y) {
   if (H.ncell == 0 || !isfinite(x) || !isfinite(y)) return H.nkey;
   const int cx = (int)fmin(floor((x - H.minx) * H.inv_cell), (double)(H.gx - 1));
   const int cy = (int)fmin(floor((y - H.miny) * H.inv_cell), (double)(H.gy - 1));
   return p * H.ncell + cx * H.gy + cy;
 }
 
-// graph insertion key of a clique vertex (tiny graphs only): first appearance of the node in
-// the edge enumeration (picker pair, a index, b index, side), get_cliques.py:33-34,135-143
+// graph insertion key of a clique vertex u (a position; tiny graphs only): first appearance
+// of the node in the edge enumeration (picker pair, a index, b index, side) in local (file)
+// order, get_cliques.py:33-34,135-143
 template <int K>
 __device__ __forceinline__ uint64_t ins_key(const FCtx<K>& c, int u) {
-  const int pu = picker_of<K>(c.pb, u);
+  const int pu = picker_of<K>(c.pp, u);
   const int bu = picker_begin<K>(c.pb, pu);
-  const int lu = u - bu;
-  for (int a = 0; a < bu; ++a) {
-    if (contains16(c.S.dst, c.S.fwd[a], c.S.fwd[a + 1], u)) {
+  const int lu = (int)c.S.citems[u] - bu;
+  for (int a = 0; a < bu; ++a) {   // lower-picker boxes in file order
+    const int ap = c.S.pos[a];
+    if (contains16(c.S.dst, c.S.fwd[ap], c.S.fwd[ap + 1], u)) {
       const int qa = picker_of<K>(c.pb, a);
       return ((uint64_t)pair_index(qa, pu, K) << 49) |
              ((uint64_t)(a - picker_begin<K>(c.pb, qa)) << 25) | ((uint64_t)lu << 1) | 1ULL;
     }
   }
-  const int d0 = c.S.dst[c.S.fwd[u]];
-  const int pd = picker_of<K>(c.pb, d0);
+  // no incoming edge: its first outgoing edge = lowest target picker, smallest file index
+  const int e0 = c.S.fwd[u], e1 = c.S.fwd[u + 1];
+  const int d0 = c.S.dst[e0];
+  const int pd = picker_of<K>(c.pp, d0);
+  const int se = lb16(c.S.dst, e0, e1, picker_end<K>(c.pp, d0));
+  int dmin = 1 << 30;
+  for (int e = e0; e < se; ++e) dmin = min(dmin, (int)c.S.citems[c.S.dst[e]]);
   return ((uint64_t)pair_index(pu, pd, K) << 49) | ((uint64_t)lu << 25) |
-         ((uint64_t)(d0 - picker_begin<K>(c.pb, pd)) << 1);
+         ((uint64_t)(dmin - picker_begin<K>(c.pb, pd)) << 1);
 }
 
 // ILP epilogue of one buffered clique (thread per clique): reference get_cliques.py:169-202.
-// j = output index; mem = local box indices in picker order.  Scores come from LDS.
+// j = output index; mem = member positions in picker order.  Main pass: COO rows, weight,
+// confidence, members and the consensus when one member has the largest weighted degree;
+// returns true when the consensus needs the node-iteration order (a degree tie, or
+// --multi_out), which fused_epilogue_order computes in a second, rarely-taken pass (its
+// 64-bit hashing stays out of this pass's register budget).
 template <int K, bool W>
-__device__ __forceinline__ void fused_epilogue(const FCtx<K>& c, int64_t j, const int (&mem)[K]) {
-  double ji[K][K], s[K], xs[K], ys[K];
+__device__ __forceinline__ bool fused_epilogue_main(const FCtx<K>& c, int64_t j,
+                                                    const int (&mem)[K]) {
+  double ji[K][K], xs[K], ys[K];
+  int li[K];   // local (file-order) indices: id order
+  {
+    double s[K];
+    int r[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      const double2 xy = ld_xy<W>(c.S, mem[i]);
+      xs[i] = xy.x;
+      ys[i] = xy.y;
+      li[i] = c.S.citems[mem[i]];
+      r[i] = c.S.vrank[mem[i]];
+    }
+    if (c.S.vstaged) {
+#pragma unroll
+      for (int i = 0; i < K; ++i) s[i] = c.S.vscore[r[i]];
+    } else {
+#pragma unroll
+      for (int i = 0; i < K; ++i) s[i] = c.score[c.b0 + li[i]];
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+      for (int q = 0; q < K - 1 - i; ++q) {
+        const int a = r[q], b = r[q + 1];
+        r[q] = min(a, b);
+        r[q + 1] = max(a, b);
+      }
+#pragma unroll
+    for (int i = 0; i < K; ++i) c.rows[j * K + i] = r[i];
+#pragma unroll
+    for (int a = 0; a < K; ++a)
+#pragma unroll
+      for (int b = a + 1; b < K; ++b) ji[a][b] = jaccard(xs[a], ys[a], xs[b], ys[b], c.B, c.two_b2);
+    float w, conf;
+    epi_weights<K>(ji, s, &w, &conf);
+    c.w[j] = w;
+    c.conf[j] = conf;
+  }
+  if (c.flags & (2 | 32)) {
+#pragma unroll
+    for (int i = 0; i < K; ++i) c.members[j * K + i] = c.b0 + li[i];
+  }
+  uint32_t top;
+  const int arg = epi_degree_max<K>(ji, &top);
+  if ((top & (top - 1)) != 0 || (c.flags & 2)) return true;
+  int cons = li[0];
+#pragma unroll
+  for (int i = 1; i < K; ++i) cons = (arg == i) ? li[i] : cons;
+  c.consensus[j] = c.b0 + cons;
+  return false;
+}
+
+// second pass for the cliques fused_epilogue_main deferred: networkx node-iteration order
+// (CPython set order or graph insertion order), consensus among the tied maximal members,
+// and the --multi_out member order
+template <int K, bool W>
+__device__ __forceinline__ void fused_epilogue_order(const FCtx<K>& c, int64_t j,
+                                                     const int (&mem)[K]) {
+  double ji[K][K], xs[K], ys[K];
+  int li[K];
   int64_t ids[K];
   uint64_t ins[K] = {};
 #pragma unroll
   for (int i = 0; i < K; ++i) {
-    const double2 xy = ld_xy<W>(c.S, c.S.pos[mem[i]]);
+    const double2 xy = ld_xy<W>(c.S, mem[i]);
     xs[i] = xy.x;
     ys[i] = xy.y;
-    s[i] = c.S.sscore[mem[i]];
-    ids[i] = c.idb + mem[i];
+    li[i] = c.S.citems[mem[i]];
+    ids[i] = c.idb + li[i];
+  }
+  if (!c.set_order) {
+    for (int i = 0; i < K; ++i) ins[i] = ins_key<K>(c, mem[i]);
   }
 #pragma unroll
   for (int a = 0; a < K; ++a)
 #pragma unroll
     for (int b = a + 1; b < K; ++b) ji[a][b] = jaccard(xs[a], ys[a], xs[b], ys[b], c.B, c.two_b2);
-  const bool multi = (c.flags & 2) != 0;
-  if (!c.set_order) {
-    for (int i = 0; i < K; ++i) ins[i] = ins_key<K>(c, mem[i]);
-  }
-  Epi<K> e;
-  epilogue<K>(mem, ji, s, xs, ys, ids, c.set_order, ins, multi, e);
-  int r[K];
+  uint32_t top;
+  int arg = epi_degree_max<K>(ji, &top);
+  const uint32_t ord = node_order<K>(li, xs, ys, ids, c.set_order, ins);
+  if ((top & (top - 1)) != 0) arg = epi_tie_arg<K>(top, ord);
+  int cons = li[0];
 #pragma unroll
-  for (int i = 0; i < K; ++i) r[i] = c.S.vrank[mem[i]];
-#pragma unroll
-  for (int i = 0; i < K; ++i)
-#pragma unroll
-    for (int q = 0; q < K - 1 - i; ++q) {
-      const int a = r[q], b = r[q + 1];
-      r[q] = min(a, b);
-      r[q + 1] = max(a, b);
-    }
-#pragma unroll
-  for (int i = 0; i < K; ++i) c.rows[j * K + i] = r[i];
-  c.w[j] = e.w;
-  c.conf[j] = e.conf;
-  int cons = mem[0];
-#pragma unroll
-  for (int i = 1; i < K; ++i) cons = (e.arg == i) ? mem[i] : cons;
+  for (int i = 1; i < K; ++i) cons = (arg == i) ? li[i] : cons;
   c.consensus[j] = c.b0 + cons;
-  if (c.flags & (2 | 32)) {
+  if (c.flags & 2) {
 #pragma unroll
-    for (int i = 0; i < K; ++i) c.members[j * K + i] = c.b0 + mem[i];
-  }
-  if (multi) {
-#pragma unroll
-    for (int i = 0; i < K; ++i) c.order[j * K + i] = (uint8_t)e.ord[i];
+    for (int i = 0; i < K; ++i) c.order[j * K + i] = (uint8_t)((ord >> (4 * i)) & 15);
   }
 }
 
@@ -293,7 +381,7 @@ struct FLevel {
     const int prev = mem[D - 1];
     const int lo = c.S.fwd[prev];
     int hi;
-    if (FILL) hi = lb16(c.S.dst, lo, c.S.fwd[prev + 1], c.pb[D + 1]);
+    if (FILL) hi = lb16(c.S.dst, lo, c.S.fwd[prev + 1], c.pp[D + 1]);
     else hi = c.S.split[prev];
     for (int e = lo; e < hi; ++e) {
       const int h = c.S.dst[e];
@@ -317,6 +405,7 @@ struct FLevel<K, K, FILL> {
         uint16_t* dstb = c.S.cbuf + (j - c.c0) * K;
 #pragma unroll
         for (int i = 0; i < K; ++i) dstb[i] = (uint16_t)mem[i];
+        c.cq_ord[j - c.c0] = 0;
       }
     } else {
       // queue the clique (members + ordinal within the root's DFS) while the queue has room;
@@ -345,7 +434,7 @@ struct Stencil {
 
 template <int K, bool W>
 __device__ __forceinline__ void stencil_setup(Stencil& st, int ts, const FShared& S,
-                                              const FusedHdr& H) {
+                                              const GridU& H) {
   const int key = S.scell[ts];
   st.a = ld_xy<W>(S, ts);
   st.p = K;
@@ -371,7 +460,7 @@ __device__ __forceinline__ void stencil_setup(Stencil& st, int ts, const FShared
 
 // column range [lo, hi) of the stencil in picker q's grid, column offset d (-1, 0, 1)
 __device__ __forceinline__ void stencil_range(const Stencil& st, const FShared& S,
-                                              const FusedHdr& H, int q, int d, int& lo, int& hi) {
+                                              const GridU& H, int q, int d, int& lo, int& hi) {
   const int col = st.cx + d;
   lo = hi = 0;
   if (col < 0 || col >= H.gx) return;
@@ -412,7 +501,7 @@ __device__ __forceinline__ bool edge_test(double2 a, double2 b, double B, double
 // candidate of a higher picker; returns the edge count and the bitmask of edge candidates
 // (candidates 0..31 in stencil order; later candidates are re-tested by the fill).
 template <int K, bool W>
-__device__ __forceinline__ int pairs_count(const Stencil& st, const FShared& S, const FusedHdr& H,
+__device__ __forceinline__ int pairs_count(const Stencil& st, const FShared& S, const GridU& H,
                                            double B, double two_b2, double i_lo, double i_hi,
                                            uint32_t* mask_out) {
   uint32_t mask = 0;
@@ -434,10 +523,11 @@ __device__ __forceinline__ int pairs_count(const Stencil& st, const FShared& S, 
   return cnt;
 }
 
-// P2 fill: write the box's forward targets at d[0..cnt) from the count's bitmask (re-testing
-// candidates past the 32nd), then sort them by target (insertion sort; lists are short).
+// P2 fill: write the box's forward targets (positions) at d[0..cnt) from the count's bitmask
+// (re-testing candidates past the 32nd).  Grids are visited in picker order and each grid's
+// column ranges in key order, so the list comes out sorted.
 template <int K, bool W>
-__device__ __forceinline__ void pairs_fill(const Stencil& st, const FShared& S, const FusedHdr& H,
+__device__ __forceinline__ void pairs_fill(const Stencil& st, const FShared& S, const GridU& H,
                                            uint32_t mask, uint16_t* d, int cnt, double B,
                                            double two_b2, double i_lo, double i_hi) {
   int c = 0, kk = 0;
@@ -453,31 +543,29 @@ __device__ __forceinline__ void pairs_fill(const Stencil& st, const FShared& S, 
         while (bits) {
           const int b = __builtin_ctz(bits);
           bits &= bits - 1;
-          d[c++] = S.citems[lo + b];
+          d[c++] = (uint16_t)(lo + b);
         }
       } else {
         for (int t = lo; t < hi; ++t) {
           const int idx = kk + (t - lo);
           const bool e = idx < 32 ? ((mask >> idx) & 1u) != 0
                                   : edge_test(st.a, ld_xy<W>(S, t), B, two_b2, i_lo, i_hi);
-          if (e) d[c++] = S.citems[t];
+          if (e) d[c++] = (uint16_t)t;
         }
       }
       kk += len;
     }
-  }
-  for (int a = 1; a < cnt; ++a) {
-    const uint16_t key = d[a];
-    int b = a - 1;
-    while (b >= 0 && d[b] > key) { d[b + 1] = d[b]; --b; }
-    d[b + 1] = key;
   }
 }
 
 // Waves per SIMD the register allocator targets.  K = 3 fits 64 VGPRs (4 small spills) for 8
 // waves per SIMD = 4 workgroups per CU, which the f32-coordinate LDS layout also allows; larger
 // K keep the compiler's choice (their VGPRs, not LDS, bound the occupancy).
+#ifdef RGC_X_NOWPE   // timing experiment: compiler's own register budget
+constexpr int fused_waves_per_eu(int) { return 1; }
+#else
 constexpr int fused_waves_per_eu(int k) { return k <= 3 ? 8 : 1; }
+#endif
 
 template <int K, bool W>
 __global__ __launch_bounds__(FWG) __attribute__((amdgpu_waves_per_eu(fused_waves_per_eu(K))))
@@ -491,6 +579,8 @@ void k_fused(FusedArgs A) {
   S.cnt = reinterpret_cast<uint32_t*>(smem + L.off_cnt);
   S.fwd = reinterpret_cast<uint16_t*>(smem + L.off_fwd);
   S.split = reinterpret_cast<uint16_t*>(smem + L.off_scell);
+  S.vscore = reinterpret_cast<double*>(smem + L.off_parent);
+  S.vstaged = false;
   S.parent = reinterpret_cast<uint32_t*>(smem + L.off_parent);
   S.citems = reinterpret_cast<uint16_t*>(smem + L.off_citems);
   S.pos = reinterpret_cast<uint16_t*>(smem + L.off_pos);
@@ -498,10 +588,8 @@ void k_fused(FusedArgs A) {
   S.vrank = reinterpret_cast<uint16_t*>(smem + L.off_vrank);
   S.flags = reinterpret_cast<uint8_t*>(smem + L.off_flags);
   S.dst = reinterpret_cast<uint16_t*>(smem + L.off_dst);
-  S.sscore = reinterpret_cast<double*>(smem + L.off_parent);
   S.cbuf = reinterpret_cast<uint16_t*>(smem + L.off_cbuf);
   const int cbuf_bytes = L.off_parent - L.off_cbuf;
-  const int cbuf_cap = cbuf_bytes / (2 * K);         // cliques per P6 re-walk chunk
   const int tid = threadIdx.x;
   const int m = A.mg_list ? A.mg_list[blockIdx.x] : (int)blockIdx.x;
 #ifdef RGC_STAMPS
@@ -609,6 +697,7 @@ void k_fused(FusedArgs A) {
   if (tid == 0) {
     H.minx = mnx; H.miny = mny; H.cell = A.B; H.inv_cell = 0.0; H.gx = 0; H.gy = 0; H.ncell = 0;
     H.status = 0; H.C = 0; H.base = 0; H.V = 0; H.target = -1; H.ccur = 0;
+    H.tief[0] = H.tief[1] = 0;
     if (mnx <= mxx && A.B > 0.0) {
       const double ex = mxx - mnx, ey = mxy - mny;
       if (!(ex < 0x1p40 && ey < 0x1p40)) {
@@ -635,40 +724,56 @@ void k_fused(FusedArgs A) {
     H.xbs = (mnx < mxx && ex < 0x1p60) ? (double)n / ex : 0.0;
   }
   __syncthreads();
-  const int nk = H.nkey;
+  const GridU G = grid_u(H);
+  const int nk = G.nkey;
   // counting sort by key with packed u16 counters (two keys per LDS word)
   uint32_t* cw = reinterpret_cast<uint32_t*>(S.cstart);
   for (int q = tid; q <= (nk + 2) / 2; q += FWG) cw[q] = 0;
-  // union-find / node flags / CC-size counters for the P2 fill (parent, flags, smark and vrank
-  // are untouched until then)
-  uint32_t* ccsz = reinterpret_cast<uint32_t*>(S.vrank);   // packed u16 CC sizes
+  // union-find and node flags for the P2 fill (by position; untouched until then)
   for (int i = tid; i < n; i += FWG) {
     S.parent[i] = i;
     S.flags[i] = 0;
   }
-  for (int q = tid; q < (n + 1) / 2; q += FWG) ccsz[q] = 0;
   __syncthreads();
   // counts go to slot key + 1, so the exclusive scan leaves bucket q's start in slot q + 1;
   // the scatter's cursors advance it to bucket q's end = bucket q+1's start, which leaves
   // cstart[q] = start of bucket q for q = 0..nk+1 with no rebuild pass.  The key waits in
   // pos[i] between the two passes.
   each_box([&](int i, double xv, double yv) {
-    const int q = box_key(H, picker_of<K>(c.pb, i), xv, yv) + 1;
+    const int q = box_key(G, picker_of<K>(c.pb, i), xv, yv) + 1;
     S.pos[i] = (uint16_t)q;
     atomicAdd(&cw[q >> 1], 1u << (16 * (q & 1)));
   });
   __syncthreads();
   block_scan_u16<FWG>(S.cstart, nk + 2, H.red64);
-  each_box([&](int i, double xv, double yv) {
+  each_box([&](int i, double, double) {
     const int q = S.pos[i];
     const int sh = 16 * (q & 1);
     const int t = (atomicAdd(&cw[q >> 1], 1u << sh) >> sh) & 0xFFFF;
+    S.citems[t] = (uint16_t)i;   // arrival order, made deterministic below
+  });
+  __syncthreads();
+  // deterministic order inside each bucket: by local index (buckets hold a few boxes)
+  uint16_t* tpos = S.vrank;   // final position of each box (vrank is free until P2)
+  each_box([&](int i, double, double) {
+    const int q = S.pos[i];
+    const int lo = S.cstart[q - 1], hi = S.cstart[q];
+    int t = lo;
+    for (int u = lo; u < hi; ++u) t += (int)S.citems[u] < i ? 1 : 0;
+    tpos[i] = (uint16_t)t;
+  });
+  __syncthreads();
+  each_box([&](int i, double xv, double yv) {
+    const int t = tpos[i];
+    S.scell[t] = (uint16_t)(S.pos[i] - 1);
     S.citems[t] = (uint16_t)i;
     S.pos[i] = (uint16_t)t;
-    S.scell[t] = (uint16_t)(q - 1);
     st_xy<W>(S, t, xv, yv);
   });
   __syncthreads();
+  // picker bounds in position space: grid p occupies [pp[p], pp[p+1]); non-finite boxes follow
+#pragma unroll
+  for (int p = 0; p <= K; ++p) c.pp[p] = ufl(S.cstart[p * G.ncell]);
 
   STOP_AFTER(1);
   STAMP(2);
@@ -685,11 +790,13 @@ void k_fused(FusedArgs A) {
   // so their stencils overlap (similar trip counts, broadcast LDS reads), and the waves of
   // picker K-1 have nothing to do.  cnt[] (dead until P3) keeps
   // each box's edge bitmask for the fill.
+  uint32_t* ccsz = reinterpret_cast<uint32_t*>(S.vrank);   // packed u16 CC sizes (P2-P3)
+  for (int q = tid; q < (n + 1) / 2; q += FWG) ccsz[q] = 0;
   for (int ts = tid; ts < n; ts += FWG) {
     Stencil st;
-    stencil_setup<K, W>(st, ts, S, H);
+    stencil_setup<K, W>(st, ts, S, G);
     uint32_t mask;
-    S.fwd[S.citems[ts]] = (uint16_t)pairs_count<K, W>(st, S, H, B, two_b2, i_lo, i_hi, &mask);
+    S.fwd[ts] = (uint16_t)pairs_count<K, W>(st, S, G, B, two_b2, i_lo, i_hi, &mask);
     S.cnt[ts] = mask;
   }
   __syncthreads();
@@ -707,14 +814,17 @@ void k_fused(FusedArgs A) {
   if (H.status == 0) {
     // fill + sort each list, then union its edges (lock-free union-find, P3's first half)
     for (int ts = tid; ts < n; ts += FWG) {
-      const int i = S.citems[ts];
+      const int i = ts;
       const int base = S.fwd[i], cnt = (int)S.fwd[i + 1] - base;
       if (cnt == 0) continue;
       Stencil st;
-      stencil_setup<K, W>(st, ts, S, H);
+      stencil_setup<K, W>(st, ts, S, G);
       uint16_t* d = S.dst + base;
-      pairs_fill<K, W>(st, S, H, S.cnt[ts], d, cnt, B, two_b2, i_lo, i_hi);
+      pairs_fill<K, W>(st, S, G, S.cnt[ts], d, cnt, B, two_b2, i_lo, i_hi);
       S.flags[i] = 1;
+#ifdef RGC_X_NOUNION
+      continue;   // timing experiment only (wrong CC outputs)
+#endif
       for (int e = 0; e < cnt; ++e) {
         const uint32_t h = d[e];
         S.flags[h] = 1;
@@ -749,7 +859,7 @@ void k_fused(FusedArgs A) {
   for (int i = tid; i < n; i += FWG) {
     if (!S.flags[i]) continue;
     const int e0 = S.fwd[i], e1 = S.fwd[i + 1];
-    S.split[i] = (uint16_t)lb16(S.dst, e0, e1, next_picker_end<K>(c.pb, i));   // every node
+    S.split[i] = (uint16_t)lb16(S.dst, e0, e1, next_picker_end<K>(c.pp, i));   // every node
     const uint32_t r = uf_find_lds(S.parent, i);
     lds_st(S.parent + i, r);
     atomicAdd(&ccsz[r >> 1], 1u << (16 * (r & 1)));
@@ -790,12 +900,17 @@ void k_fused(FusedArgs A) {
       if (e0 == e1) continue;
       const uint32_t r = S.parent[i];
       if (cc_size(r) != H.cc_max) continue;
-      const int pi = picker_of<K>(c.pb, i);
-      const int h = S.dst[e0];   // lists are sorted: the first target is the smallest key
-      const int ph = picker_of<K>(c.pb, h);
+      // the box's first edge in enumeration order: lowest target picker (the first segment
+      // of the position-sorted list), smallest file index inside it
+      const int pi = picker_of<K>(c.pp, i);
+      const int h0 = S.dst[e0];
+      const int ph = picker_of<K>(c.pp, h0);
+      const int se = lb16(S.dst, e0, e1, picker_end<K>(c.pp, h0));
+      int hmin = 1 << 30;
+      for (int e = e0; e < se; ++e) hmin = min(hmin, (int)S.citems[S.dst[e]]);
       const uint64_t key = ((uint64_t)pair_index(pi, ph, K) << 48) |
-                           ((uint64_t)(i - picker_begin<K>(c.pb, pi)) << 32) |
-                           ((uint64_t)(h - picker_begin<K>(c.pb, ph)) << 16) | r;
+                           ((uint64_t)(S.citems[i] - picker_begin<K>(c.pb, pi)) << 32) |
+                           ((uint64_t)(hmin - picker_begin<K>(c.pb, ph)) << 16) | r;
       best = key < best ? key : best;
     }
     best = block_min_u64<FWG>(best, H.redu);
@@ -810,7 +925,7 @@ void k_fused(FusedArgs A) {
   c.cq_cap = cbuf_bytes / (2 * K + 2);
   c.cq_ord = S.cbuf + c.cq_cap * K;
   c.ccur = &H.ccur;
-  const int n0 = c.pb[1];
+  const int n0 = c.pp[1];   // roots: picker-0 positions
   const int target = H.target;
   for (int r = tid; r < n0; r += FWG) {
     uint32_t cntr = 0;
@@ -853,22 +968,20 @@ void k_fused(FusedArgs A) {
     for (int q = tid; q <= n; q += FWG) bcnt[q] = 0;
     __syncthreads();
     for (int t = tid; t < n; t += FWG) {
-      const int vi = S.citems[t];
-      if (S.flags[vi] != 3) continue;
-      S.vrank[vi] = (uint16_t)atomicAdd(&bcnt[xbucket(ld_xy<W>(S, t).x)], 1u);
+      if (S.flags[t] != 3) continue;
+      S.vrank[t] = (uint16_t)atomicAdd(&bcnt[xbucket(ld_xy<W>(S, t).x)], 1u);
     }
     __syncthreads();
     const int64_t V = block_scan_array<FWG>(bcnt, n, H.red64);
     if (tid == 0) { H.V = (int)V; bcnt[n] = (uint32_t)V; }
     for (int t = tid; t < n; t += FWG) {
-      const int vi = S.citems[t];
-      if (S.flags[vi] != 3) continue;
-      blist[bcnt[xbucket(ld_xy<W>(S, t).x)] + S.vrank[vi]] = (uint16_t)t;
+      if (S.flags[t] != 3) continue;
+      blist[bcnt[xbucket(ld_xy<W>(S, t).x)] + S.vrank[t]] = (uint16_t)t;
     }
     __syncthreads();
     for (int t = tid; t < n; t += FWG) {
+      if (S.flags[t] != 3) continue;
       const int vi = S.citems[t];
-      if (S.flags[vi] != 3) continue;
       const double2 v = ld_xy<W>(S, t);
       const int b = xbucket(v.x);
       const int lo = bcnt[b], hi = bcnt[b + 1];
@@ -879,7 +992,7 @@ void k_fused(FusedArgs A) {
         const int ui = S.citems[tu];
         rk += (w.x < v.x) || (w.x == v.x && (w.y < v.y || (w.y == v.y && ui < vi)));
       }
-      S.vrank[vi] = (uint16_t)rk;
+      S.vrank[t] = (uint16_t)rk;
     }
     __syncthreads();
 
@@ -889,23 +1002,26 @@ void k_fused(FusedArgs A) {
     // one thread per clique (coalesced output stores).  Cliques come from the P4 queue, whose
     // output index is (root's scanned offset + ordinal within the root): the same order as a
     // sequential root-by-root walk.  Micrographs whose cliques overflowed the queue re-walk
-    // the DFS per chunk of <= cbuf_cap cliques.
-    for (int i = tid; i < n; i += FWG)
-      if (S.flags[i] == 3) S.sscore[i] = c.score[b0 + i];
-    __syncthreads();
+    // the DFS per chunk of <= cq_cap cliques.
+    // scores of the clique vertices into LDS by row rank when they fit in parent..scell
+    c.S.vstaged = 8 * H.V <= L.off_citems - L.off_parent;
+    if (c.S.vstaged) {
+      for (int t = tid; t < n; t += FWG)
+        if (S.flags[t] == 3) c.S.vscore[S.vrank[t]] = c.score[b0 + S.citems[t]];
+      __syncthreads();
+    }
     STAMP(11);  // score staging
+    // per chunk of queued cliques: main pass (thread per clique), then the order pass over
+    // the cliques it flagged (bit 15 of the slot's ordinal word; the slot's output index is
+    // kept in the low bits).  Micrographs whose cliques overflowed the queue re-walk the DFS
+    // per chunk of <= cq_cap cliques into the same buffer.
     const int64_t Cm = H.C;
-    if (Cm <= c.cq_cap) {
-      for (int64_t sl = tid; sl < Cm; sl += FWG) {
-        int mem[K];
-        const uint16_t* sb = S.cbuf + sl * K;
-#pragma unroll
-        for (int i = 0; i < K; ++i) mem[i] = sb[i];
-        fused_epilogue<K, W>(c, H.base + S.cnt[mem[0]] + c.cq_ord[sl], mem);
-      }
-    } else {
-      for (int64_t c0 = 0; c0 < Cm; c0 += cbuf_cap) {
-        const int64_t c1 = min(Cm, c0 + (int64_t)cbuf_cap);
+    const bool queued = Cm <= c.cq_cap;
+    int ci = 0;
+    for (int64_t c0 = 0; c0 < Cm; c0 += c.cq_cap, ++ci) {
+      const int64_t c1 = min(Cm, c0 + (int64_t)c.cq_cap);
+      if (tid == 0) H.tief[(ci + 1) & 1] = 0;   // last read before the previous chunk's end
+      if (!queued) {
         c.c0 = c0;
         c.c1 = c1;
         for (int r = tid; r < n0; r += FWG) {
@@ -917,15 +1033,34 @@ void k_fused(FusedArgs A) {
           FLevel<K, 1, true>::run(c, mem);
         }
         __syncthreads();
-        for (int64_t j = c0 + tid; j < c1; j += FWG) {
+      }
+      bool any = false;
+      for (int64_t sl = tid; sl < c1 - c0; sl += FWG) {
+        int mem[K];
+        const uint16_t* sb = S.cbuf + sl * K;
+#pragma unroll
+        for (int i = 0; i < K; ++i) mem[i] = sb[i];
+        const int64_t j = queued ? S.cnt[mem[0]] + c.cq_ord[sl] : c0 + sl;
+        if (fused_epilogue_main<K, W>(c, H.base + j, mem)) {
+          c.cq_ord[sl] |= 0x8000;
+          any = true;
+        }
+      }
+      if (any) H.tief[ci & 1] = 1;
+      __syncthreads();
+      if (H.tief[ci & 1]) {
+        for (int64_t sl = tid; sl < c1 - c0; sl += FWG) {
+          const uint32_t o = c.cq_ord[sl];
+          if (!(o & 0x8000)) continue;
           int mem[K];
-          const uint16_t* sb = S.cbuf + (j - c0) * K;
+          const uint16_t* sb = S.cbuf + sl * K;
 #pragma unroll
           for (int i = 0; i < K; ++i) mem[i] = sb[i];
-          fused_epilogue<K, W>(c, H.base + j, mem);
+          const int64_t j = queued ? S.cnt[mem[0]] + (o & 0x7FFF) : c0 + sl;
+          fused_epilogue_order<K, W>(c, H.base + j, mem);
         }
-        __syncthreads();
       }
+      __syncthreads();
     }
   }
   STAMP(12);
@@ -948,13 +1083,13 @@ template <int K, bool W>
 static int launch_fused_t(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArgs& A) {
   static bool attr_set = false;
   if (!attr_set) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused<K, W>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-      return -2;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused<K, W>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
   hipLaunchKernelGGL((k_fused<K, W>), dim3(n_blocks), dim3(FWG), lds_bytes, stream, A);
-  return 0;
+  return (int)hipGetLastError();
 }
 
 template <int K, bool W>
