@@ -13,6 +13,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -50,7 +51,7 @@ namespace {
 
 enum DevBufId {
   // fused path / whole batch
-  D_FBOXOFF, D_FIDBASE, D_MGLIST, D_FSTAT, D_CURSOR, D_X, D_Y, D_S,
+  D_FBOXOFF, D_FIDBASE, D_MGLIST, D_MGOUT, D_CURSOR, D_X, D_Y, D_S,
   // outputs
   D_ROWS, D_W, D_CONF, D_CONS, D_MEMBERS, D_ORDER,
   // multi-kernel path (sub-batch)
@@ -61,7 +62,7 @@ enum DevBufId {
   D_COUNT
 };
 enum HostBufId {
-  H_FSTAGE, H_STAGE, H_TOTAL, H_FSTAT, H_STAT, H_MGOFF, H_ROWS, H_W, H_CONF, H_CONS, H_MEMBERS,
+  H_FSTAGE, H_STAGE, H_TOTAL, H_MGOUT, H_STAT, H_MGOFF, H_ROWS, H_W, H_CONF, H_CONS, H_MEMBERS,
   H_ORDER, H_COUNT
 };
 
@@ -151,9 +152,6 @@ struct rgc_ctx {
   std::vector<const char*> time_names;
   int64_t cap_cliques = 0;   // capacity of the per-clique output arrays
   std::vector<uint64_t> stamps;   // diagnostic build only
-  // per-micrograph host outputs
-  std::vector<int32_t> status, cc_max, cc_cnt, n_nodes, n_vert;
-  std::vector<int64_t> n_edges_mg, clique_base, clique_cnt;
 };
 
 static int ensure_dev(rgc_ctx* c, int id, size_t bytes, size_t keep = 0) {
@@ -399,27 +397,25 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   c->timing = (flags & RGC_F_TIMING) != 0;
   c->n_ev = 0;
 
-  c->status.assign(n_mg, 0);
-  c->cc_max.assign(n_mg, 0);
-  c->cc_cnt.assign(n_mg, 0);
-  c->n_nodes.assign(n_mg, 0);
-  c->n_vert.assign(n_mg, 0);
-  c->n_edges_mg.assign(n_mg, 0);
-  c->clique_base.assign(n_mg, 0);
-  c->clique_cnt.assign(n_mg, 0);
+  // per-micrograph outputs: pinned SoA block, filled by one copy of the device mirror
+  TRY(ensure_host(c, H_MGOUT, mgout_bytes(n_mg)));
+  TRY(ensure_dev(c, D_MGOUT, mgout_bytes(n_mg)));
+  const MgOut ho = mgout_bind(H<void>(c, H_MGOUT), n_mg);
+  const MgOut dout = mgout_bind(D<void>(c, D_MGOUT), n_mg);
   std::memset(out, 0, sizeof(*out));
-  out->status = c->status.data();
-  out->cc_max = c->cc_max.data();
-  out->cc_cnt = c->cc_cnt.data();
-  out->n_nodes = c->n_nodes.data();
-  out->n_vert = c->n_vert.data();
-  out->n_edges_mg = c->n_edges_mg.data();
-  out->clique_base = c->clique_base.data();
-  out->clique_cnt = c->clique_cnt.data();
+  out->status = ho.status;
+  out->cc_max = ho.cc_max;
+  out->cc_cnt = ho.cc_cnt;
+  out->n_nodes = ho.n_nodes;
+  out->n_vert = ho.n_vert;
+  out->n_edges_mg = ho.n_edges;
+  out->clique_base = ho.clique_base;
+  out->clique_cnt = ho.clique_cnt;
   out->n_boxes = N;
   if (n_mg == 0) return 0;
   if (k == 1) {  // no picker pairs -> no edges -> reference ValueError on every micrograph
-    std::fill(c->status.begin(), c->status.end(), RGC_NO_EDGES);
+    std::memset(H<void>(c, H_MGOUT), 0, mgout_bytes(n_mg));
+    std::fill(ho.status, ho.status + n_mg, RGC_NO_EDGES);
     return 0;
   }
   hipStream_t s = c->stream;
@@ -439,9 +435,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   TRY(ensure_dev(c, D_FBOXOFF, nbo * 4));
   TRY(ensure_dev(c, D_FIDBASE, n_mg * 8));
   TRY(ensure_dev(c, D_MGLIST, 3 * (size_t)n_mg * 4 + 4));
-  TRY(ensure_dev(c, D_FSTAT, n_mg * sizeof(MgStat)));
   TRY(ensure_dev(c, D_CURSOR, 16));
-  TRY(ensure_host(c, H_FSTAT, n_mg * sizeof(MgStat)));
   TRY(ensure_host(c, H_TOTAL, 16));
   TRY(mark(c, "h2d_meta"));
   HIPCHK(hipMemcpyAsync(D<void>(c, D_FBOXOFF), f_bo, nbo * 4, hipMemcpyHostToDevice, s));
@@ -462,12 +456,14 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   // micrographs it deferred (coordinates not exact in f32, or more edges than its ecap) with
   // f64 coordinates; pass 2: the edge-capacity overflows of pass 1 with the whole LDS.  What
   // is still deferred (or too large for LDS) runs through the multi-kernel path.
-  std::vector<MgStat> st(n_mg);
   int64_t fused_total = 0;
   int64_t E_total = 0;
   std::vector<int32_t> deferred;
   std::vector<int32_t> todo0;
-  std::vector<int32_t> mg_class(n_mg);
+  auto mg_class = [&](int m) {
+    const int64_t nm = in->box_off[(int64_t)(m + 1) * k] - in->box_off[(int64_t)m * k];
+    return nm <= 65535 ? fused_class(nm) : 0;
+  };
   // per-call plan lookup: few distinct classes, so a linear list beats the shared memo
   std::vector<std::pair<int, const FusedPlan*>> local_plans;
   auto plan_of = [&](int pass, int cl) -> const FusedPlan& {
@@ -477,13 +473,26 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
     local_plans.push_back({key, &cached_plan(k, pass, cl)});
     return *local_plans.back().second;
   };
+  // fast path: every micrograph fits pass 0 and the largest class runs at the occupancy of
+  // the smallest (feasibility and occupancy are monotone in n) -> one launch over all of them
+  int64_t nmin = INT64_MAX, nmaxb = 0;
   for (int m = 0; m < n_mg; ++m) {
     const int64_t nm = in->box_off[(int64_t)(m + 1) * k] - in->box_off[(int64_t)m * k];
-    mg_class[m] = nm <= 65535 ? fused_class(nm) : 0;
-    if (!no_fused && mg_class[m] && plan_of(0, mg_class[m]).nmax) todo0.push_back(m);
-    else deferred.push_back(m);
+    nmin = std::min(nmin, nm);
+    nmaxb = std::max(nmaxb, nm);
   }
-  if (!todo0.empty()) {
+  const bool all0 = !no_fused && n_mg > 0 && nmaxb <= 65535 &&
+                    plan_of(0, fused_class(nmaxb)).nmax &&
+                    plan_of(0, fused_class(nmin)).wg == plan_of(0, fused_class(nmaxb)).wg;
+  if (!all0) {
+    todo0.reserve(n_mg);
+    for (int m = 0; m < n_mg; ++m) {
+      const int cl = mg_class(m);
+      if (!no_fused && cl && plan_of(0, cl).nmax) todo0.push_back(m);
+      else deferred.push_back(m);
+    }
+  }
+  if (all0 || !todo0.empty()) {
     if (c->cap_cliques < 4096) c->cap_cliques = std::max<int64_t>(4096, N);
     for (int attempt = 0; attempt < 2; ++attempt) {
       TRY(ensure_outputs(c, c->cap_cliques, 0, k, want_members, multi != 0));
@@ -492,7 +501,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
       A.k = k; A.flags = get_cc | (multi << 1) | (want_members ? 32 : 0);
       A.B = B; A.two_b2 = two_b2;
       A.box_off = D<int32_t>(c, D_FBOXOFF); A.id_base = D<int64_t>(c, D_FIDBASE);
-      A.x = x; A.y = y; A.score = sc; A.st = D<MgStat>(c, D_FSTAT);
+      A.x = x; A.y = y; A.score = sc; A.o = dout;
       A.cursor = D<unsigned long long>(c, D_CURSOR); A.cap = c->cap_cliques;
       A.rows = D<int32_t>(c, D_ROWS); A.w = D<float>(c, D_W); A.conf = D<float>(c, D_CONF);
       A.consensus = D<int32_t>(c, D_CONS);
@@ -506,15 +515,20 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
       std::vector<int32_t> todo = todo0, left;
       int ml_off = 0;   // mg-list slots used (earlier passes' lists stay intact)
       bool overflow = false;
-      for (int pass = 0; pass < 3 && !todo.empty(); ++pass) {
+      for (int pass = 0; pass < 3 && (!todo.empty() || (pass == 0 && all0)); ++pass) {
         const bool wide = pass > 0;
+        const bool single = pass == 0 && all0;   // identity list: block b = micrograph b
         // bucket by size class (few classes: linear search of the bucket keys)
         std::vector<int> keys;
         std::vector<std::vector<int32_t>> lists;
         left.clear();
+        if (single) {
+          keys.assign(1, fused_class(nmaxb));
+          lists.assign(1, std::vector<int32_t>());
+        }
         int last = -1;
         for (int32_t m : todo) {
-          const int cl = mg_class[m];
+          const int cl = mg_class(m);
           if (!cl || !plan_of(pass, cl).nmax) { left.push_back(m); continue; }
           if (last < 0 || keys[last] != cl) {
             last = -1;
@@ -526,21 +540,9 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
         }
         std::vector<int32_t> by;
         std::vector<size_t> starts;
-        // every micrograph in one launch (identity list) when the largest class runs at the
-        // occupancy of every smaller one: no list upload, no tail per class
-        bool single = pass == 0 && (int)todo.size() == n_mg && left.empty() && !keys.empty();
         if (single) {
-          int cmax = 0;
-          for (int cl : keys) cmax = std::max(cmax, cl);
-          for (int cl : keys) single = single && plan_of(0, cl).wg == plan_of(0, cmax).wg;
-          if (single) {
-            keys.assign(1, cmax);
-            lists.assign(1, std::vector<int32_t>());
-            by = todo;
-            starts.push_back(0);
-          }
-        }
-        if (!single) {
+          starts.push_back(0);
+        } else {
           for (size_t q = 0; q < keys.size(); ++q) {
             starts.push_back(by.size());
             by.insert(by.end(), lists[q].begin(), lists[q].end());
@@ -567,26 +569,32 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
                         (le > 0 ? hipGetErrorString((hipError_t)le) : "unsupported k"));
         }
         TRY(mark(c, "d2h_stats"));
-        HIPCHK(hipMemcpyAsync(H<void>(c, H_FSTAT), D<void>(c, D_FSTAT), n_mg * sizeof(MgStat),
+        HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOUT), D<void>(c, D_MGOUT), mgout_bytes(n_mg),
                               hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(H<void>(c, H_TOTAL), D<void>(c, D_CURSOR), 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(H<void>(c, H_TOTAL), D<void>(c, D_CURSOR), 16, hipMemcpyDeviceToHost, s));
         HIPCHK(hipGetLastError());
         HIPCHK(hipStreamSynchronize(s));
-        const MgStat* fs = H<MgStat>(c, H_FSTAT);
+        const int32_t* fst = ho.status;
         ml_off += (int)by.size();
         todo.clear();
-        for (const int32_t m : by) {
-          st[m] = fs[m];
-          if (fs[m].status == RGC_ST_OVERFLOW) overflow = true;
-          else if (fs[m].status == RGC_ST_DEFER_WIDE || fs[m].status == RGC_ST_DEFER) todo.push_back(m);
+        auto check = [&](int32_t m) {
+          const int stt = fst[m];
+          if (stt == RGC_ST_OVERFLOW) overflow = true;
+          else if (stt == RGC_ST_DEFER_WIDE || stt == RGC_ST_DEFER) todo.push_back(m);
+        };
+        if (single) {
+          for (int32_t m = 0; m < n_mg; ++m)
+            if (fst[m] >= RGC_ST_DEFER) check(m);
+        } else {
+          for (const int32_t m : by) check(m);
         }
         for (int32_t m : left) todo.push_back(m);
       }
       fused_total = (int64_t)H<unsigned long long>(c, H_TOTAL)[0];
 #ifdef RGC_STAMPS
-      c->stamps.resize((size_t)todo0.size() * 16);   // pass 0's workgroups
-      HIPCHK(hipMemcpy(c->stamps.data(), D<void>(c, D_STAMPS), todo0.size() * 128,
-                       hipMemcpyDeviceToHost));
+      const size_t n0w = all0 ? (size_t)n_mg : todo0.size();   // pass 0's workgroups
+      c->stamps.resize(n0w * 16);
+      HIPCHK(hipMemcpy(c->stamps.data(), D<void>(c, D_STAMPS), n0w * 128, hipMemcpyDeviceToHost));
 #endif
       if (!overflow && fused_total <= c->cap_cliques) {
         for (int32_t m : todo) deferred.push_back(m);
@@ -596,10 +604,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
       c->cap_cliques = fused_total + fused_total / 8 + 1024;   // grow and re-run once
       c->n_ev = 0;
     }
-    for (int32_t m : todo0) {
-      const int stt = st[m].status;
-      if (stt != RGC_ST_DEFER && stt != RGC_ST_DEFER_WIDE) E_total += st[m].n_edges;
-    }
+    E_total = (int64_t)H<unsigned long long>(c, H_TOTAL)[1];   // finished micrographs
   }
 
   int64_t C_total = fused_total;
@@ -640,7 +645,20 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
     TRY(mark(c, "k_remap"));
     launch_remap(s, Cm, k, D<int32_t>(c, D_ORIG), D<int32_t>(c, D_CONS) + fused_total,
                  D<int32_t>(c, D_MEMBERS) + fused_total * k);
-    for (int i = 0; i < ns; ++i) st[deferred[i]] = sst[i];
+    for (int i = 0; i < ns; ++i) {
+      const int m = deferred[i];
+      const MgStat& t = sst[i];
+      int stt = t.status;
+      if (stt == RGC_OK && t.clique_cnt == 0) stt = RGC_NO_CLIQUES;
+      ho.status[m] = stt;
+      ho.cc_max[m] = t.cc_max;
+      ho.cc_cnt[m] = t.cc_cnt;
+      ho.n_nodes[m] = t.n_nodes;
+      ho.n_vert[m] = t.n_vert;
+      ho.n_edges[m] = t.n_edges;
+      ho.clique_base[m] = t.clique_base;
+      ho.clique_cnt[m] = stt == RGC_OK ? t.clique_cnt : 0;
+    }
     C_total += Cm;
     E_total += Em;
   }
@@ -685,18 +703,6 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
 
-  for (int m = 0; m < n_mg; ++m) {
-    int stt = st[m].status;
-    if (stt == RGC_OK && st[m].clique_cnt == 0) stt = RGC_NO_CLIQUES;
-    c->status[m] = stt;
-    c->cc_max[m] = st[m].cc_max;
-    c->cc_cnt[m] = st[m].cc_cnt;
-    c->n_nodes[m] = st[m].n_nodes;
-    c->n_vert[m] = st[m].n_vert;
-    c->n_edges_mg[m] = st[m].n_edges;
-    c->clique_base[m] = st[m].clique_base;
-    c->clique_cnt[m] = stt == RGC_OK ? st[m].clique_cnt : 0;
-  }
 
   if (c->timing) {
     c->times.clear();

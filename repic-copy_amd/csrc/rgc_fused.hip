@@ -558,6 +558,23 @@ __device__ __forceinline__ void pairs_fill(const Stencil& st, const FShared& S, 
   }
 }
 
+// per-micrograph results of workgroup thread 0; finished micrographs add their edges to the
+// batch total (deferred ones are counted by the pass that finishes them)
+__device__ __forceinline__ void put_stats(const FusedArgs& A, int m, int status, int64_t edges,
+                                          int nodes, int cc_cnt, int cc_max, int V, int64_t base,
+                                          int64_t C) {
+  A.o.status[m] = status;
+  A.o.cc_max[m] = cc_max;
+  A.o.cc_cnt[m] = cc_cnt;
+  A.o.n_nodes[m] = nodes;
+  A.o.n_vert[m] = V;
+  A.o.n_edges[m] = edges;
+  A.o.clique_base[m] = base;
+  A.o.clique_cnt[m] = C;
+  if (status == 0 || status == RGC_ST_NO_CLIQUES || status == RGC_ST_NO_EDGES)
+    atomicAdd(A.cursor + 1, (unsigned long long)edges);
+}
+
 // Waves per SIMD the register allocator targets.  K = 3 fits 64 VGPRs (4 small spills) for 8
 // waves per SIMD = 4 workgroups per CU, which the f32-coordinate LDS layout also allows; larger
 // K keep the compiler's choice (their VGPRs, not LDS, bound the occupancy).
@@ -609,7 +626,7 @@ void k_fused(FusedArgs A) {
 #define STOP_AFTER(ph)                            \
   do {                                            \
     if ((ph) == RGC_STOP_AFTER) {                 \
-      if (tid == 0) A.st[m] = MgStat{};           \
+      if (tid == 0) put_stats(A, m, 0, 0, 0, 0, 0, 0, 0, 0); \
       return;                                     \
     }                                             \
   } while (0)
@@ -679,12 +696,7 @@ void k_fused(FusedArgs A) {
     mnx = v[0]; mny = v[1]; mxx = -v[2]; mxy = -v[3];
   }
   if (!W && mnx == -INFINITY) {   // needs the f64 layout: the host relaunches it wide
-    if (tid == 0) {
-      MgStat st = {};
-      st.status = RGC_ST_DEFER_WIDE;
-      st.target = -1;
-      A.st[m] = st;
-    }
+    if (tid == 0) put_stats(A, m, RGC_ST_DEFER_WIDE, 0, 0, 0, 0, 0, 0, 0);
     return;
   }
 
@@ -842,13 +854,7 @@ void k_fused(FusedArgs A) {
     STAMP(5);   // fill + sort
   }
   if (H.status != 0) {
-    if (tid == 0) {
-      MgStat st = {};
-      st.n_edges = H.E;
-      st.status = H.status;
-      st.target = -1;
-      A.st[m] = st;
-    }
+    if (tid == 0) put_stats(A, m, H.status, H.E, 0, 0, 0, 0, 0, 0);
     return;
   }
 
@@ -1064,19 +1070,8 @@ void k_fused(FusedArgs A) {
     }
   }
   STAMP(12);
-  if (tid == 0) {
-    MgStat st = {};
-    st.n_edges = H.E;
-    st.n_nodes = H.nodes;
-    st.cc_cnt = H.cc_cnt;
-    st.cc_max = H.cc_max;
-    st.status = H.status;
-    st.target = H.target;
-    st.n_vert = H.V;
-    st.clique_base = H.base;
-    st.clique_cnt = H.C;
-    A.st[m] = st;
-  }
+  if (tid == 0)
+    put_stats(A, m, H.status, H.E, H.nodes, H.cc_cnt, H.cc_max, H.V, H.base, H.C);
 }
 
 template <int K, bool W>

@@ -36,6 +36,34 @@ struct FusedLayout {
       off_citems, off_scell, off_flags, off_smark, off_cbuf, total;
 };
 
+// Per-micrograph outputs of the fused kernel, SoA (the pinned host mirror has the same layout,
+// so one copy hands them to the caller).  mgout_bytes / mgout_bind define the layout.
+struct MgOut {
+  int32_t* status;
+  int32_t* cc_max;
+  int32_t* cc_cnt;
+  int32_t* n_nodes;
+  int32_t* n_vert;
+  int64_t* n_edges;
+  int64_t* clique_base;
+  int64_t* clique_cnt;
+};
+inline size_t mgout_bytes(int n_mg) { return (size_t)n_mg * 20 + 8 + (size_t)n_mg * 24; }
+inline MgOut mgout_bind(void* base, int n_mg) {
+  char* p = static_cast<char*>(base);
+  MgOut o;
+  o.status = reinterpret_cast<int32_t*>(p);
+  o.cc_max = o.status + n_mg;
+  o.cc_cnt = o.cc_max + n_mg;
+  o.n_nodes = o.cc_cnt + n_mg;
+  o.n_vert = o.n_nodes + n_mg;
+  char* q = p + (((size_t)n_mg * 20 + 7) & ~(size_t)7);
+  o.n_edges = reinterpret_cast<int64_t*>(q);
+  o.clique_base = o.n_edges + n_mg;
+  o.clique_cnt = o.clique_base + n_mg;
+  return o;
+}
+
 struct FusedArgs {
   int k, flags;                 // flags: bit0 get_cc, bit1 multi_out, bit5 members
   double B, two_b2;
@@ -46,8 +74,8 @@ struct FusedArgs {
   const double* x;
   const double* y;
   const double* score;
-  MgStat* st;
-  unsigned long long* cursor;   // clique-range reservation counter
+  MgOut o;                      // per-micrograph outputs (device)
+  unsigned long long* cursor;   // [0] clique-range reservation, [1] edges of finished mgs
   int64_t cap;                  // clique capacity of the output arrays
   int32_t* rows;
   float* w;
