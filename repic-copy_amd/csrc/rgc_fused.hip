@@ -606,7 +606,6 @@ void k_fused(FusedArgs A) {
   S.flags = reinterpret_cast<uint8_t*>(smem + L.off_flags);
   S.dst = reinterpret_cast<uint16_t*>(smem + L.off_dst);
   S.cbuf = reinterpret_cast<uint16_t*>(smem + L.off_cbuf);
-  const int cbuf_bytes = L.off_parent - L.off_cbuf;
   const int tid = threadIdx.x;
   const int m = A.mg_list ? A.mg_list[blockIdx.x] : (int)blockIdx.x;
 #ifdef RGC_STAMPS
@@ -928,8 +927,15 @@ void k_fused(FusedArgs A) {
   STAMP(7);   // CC stats
   // ---- P4: clique count per picker-0 root, vertex marking, output reservation
   c.set_order = 2 * K < H.nodes;
-  c.cq_cap = cbuf_bytes / (2 * K + 2);
-  c.cq_ord = S.cbuf + c.cq_cap * K;
+  // the clique queue starts right after the E used entries of dst (dst's unused tail and the
+  // cell starts are contiguous: dst immediately precedes the cell starts in the layout)
+  {
+    const int qoff = (L.off_dst + 2 * H.E + 3) & ~3;
+    S.cbuf = reinterpret_cast<uint16_t*>(smem + qoff);
+    c.S.cbuf = S.cbuf;
+    c.cq_cap = (L.off_parent - qoff) / (2 * K + 2);
+    c.cq_ord = S.cbuf + c.cq_cap * K;
+  }
   c.ccur = &H.ccur;
   const int n0 = c.pp[1];   // roots: picker-0 positions
   const int target = H.target;
