@@ -425,6 +425,153 @@ struct FLevel<K, K, FILL> {
   }
 };
 
+// ----------------------------------------------------------------------------- P4 (BFS)
+// Level-synchronous k-clique enumeration (get_cliques.py:49-56 restated for a k-partite
+// graph).  Level D holds every D-member prefix (one member per picker 0..D-1, pairwise
+// adjacent) in lexicographic order as a tree entry (index of its parent prefix << 16 | last
+// member); level 1 is implicit (the picker-0 roots).  Expanding a level: count + 32-bit mask
+// of the valid extensions per entry (candidates = first forward segment of the last member,
+// kept if every earlier member's list contains them), workgroup scan, write pass.  Level K
+// holds the cliques (lexicographic = per-root DFS order), followed by one zeroed flag word
+// per clique; the last expansion marks the members.  All levels live in the queue region
+// q[0, qbytes); the temps of the level being expanded sit at its top.  Every prefix is one
+// thread's work, so a root's subtree no longer serialises on one lane.
+template <int K>
+struct BfsOut {
+  int64_t C;        // cliques, or -1: a level did not fit (caller falls back to the DFS)
+  int lvl[K + 1];   // byte offset in q of each level's entries (2..K)
+};
+
+template <int K, int D>
+struct BfsLevel {
+  // prefix members of entry e of level D (D members, compile-time indices only)
+  __device__ __forceinline__ static void prefix(const char* q, const int (&lvl)[K + 1],
+                                                uint32_t e, int (&mm)[K]) {
+    uint32_t ent = reinterpret_cast<const uint32_t*>(q + lvl[D])[e];
+    mm[D - 1] = (int)(ent & 0xFFFF);
+    uint32_t cur = ent >> 16;
+#pragma unroll
+    for (int d = D - 1; d >= 2; --d) {
+      ent = reinterpret_cast<const uint32_t*>(q + lvl[d])[cur];
+      mm[d - 1] = (int)(ent & 0xFFFF);
+      cur = ent >> 16;
+    }
+    mm[0] = (int)cur;
+  }
+
+  __device__ __forceinline__ static BfsOut<K> run(const FShared& S, FusedHdr& H, char* q,
+                                                  int qbytes, BfsOut<K>& out, int64_t nD, int tid) {
+    int (&lvl)[K + 1] = out.lvl;
+    // temps of this level at the top of q
+    const int tb = (qbytes - 8 * (int)(nD + 1)) & ~7;
+    if (nD > 65535 || tb < lvl[D] + 4 * (int)nD) { out.C = -1; return out; }
+    uint32_t* MK = reinterpret_cast<uint32_t*>(q + tb);
+    uint32_t* CN = MK + nD;
+    for (int e = tid; e < nD; e += FWG) {
+      int mm[K];
+      prefix(q, lvl, (uint32_t)e, mm);
+      const int m = mm[D - 1];
+      const int lo = S.fwd[m], hi = S.split[m];
+      uint32_t mask = 0, cnt = 0;
+      for (int t = lo; t < hi; ++t) {
+        const int h = S.dst[t];
+        bool ok = true;
+#pragma unroll
+        for (int d = 0; d < D - 1; ++d)
+          ok = ok && contains16(S.dst, S.fwd[mm[d]], S.fwd[mm[d] + 1], h);
+        cnt += ok ? 1u : 0u;
+        mask |= (ok && t - lo < 32) ? (1u << (t - lo)) : 0u;
+      }
+      MK[e] = mask;
+      CN[e] = cnt;
+    }
+    __syncthreads();
+    const int64_t nN = block_scan_array<FWG>(CN, (int)nD, H.red64);
+    constexpr bool last = D + 1 == K;
+    const int nb = (lvl[D] + 4 * (int)nD + 3) & ~3;   // next level starts here
+    if (nN > 65535 || nN * (last ? 6 : 4) > tb - nb) { out.C = -1; return out; }
+    for (int e = tid; e < nD; e += FWG) {
+      int mm[K];
+      prefix(q, lvl, (uint32_t)e, mm);
+      const int m = mm[D - 1];
+      const int lo = S.fwd[m], hi = S.split[m];
+      const uint32_t mask = MK[e];
+      uint32_t o = CN[e];
+      for (int t = lo; t < hi; ++t) {
+        const int h = S.dst[t];
+        bool ok;
+        if (t - lo < 32) {
+          ok = (mask >> (t - lo)) & 1u;
+        } else {
+          ok = true;
+#pragma unroll
+          for (int d = 0; d < D - 1; ++d)
+            ok = ok && contains16(S.dst, S.fwd[mm[d]], S.fwd[mm[d] + 1], h);
+        }
+        if (!ok) continue;
+        reinterpret_cast<uint32_t*>(q + nb)[o] = ((uint32_t)e << 16) | (uint32_t)h;
+        if (last) {
+#pragma unroll
+          for (int d = 0; d < K - 1; ++d) S.flags[mm[d]] = 3;
+          S.flags[h] = 3;
+          reinterpret_cast<uint16_t*>(q + nb + 4 * (int)nN)[o] = 0;
+        }
+        ++o;
+      }
+    }
+    __syncthreads();
+    lvl[D + 1] = nb;
+    if constexpr (D + 1 < K) {
+      return BfsLevel<K, D + 1>::run(S, H, q, qbytes, out, nN, tid);
+    } else {
+      out.C = nN;
+      return out;
+    }
+  }
+};
+
+template <int K>
+__device__ __forceinline__ BfsOut<K> bfs_cliques(const FShared& S, FusedHdr& H, char* q,
+                                                 int qbytes, int n0, bool get_cc, uint32_t target,
+                                                 int tid) {
+  BfsOut<K> out;
+  out.C = -1;
+#pragma unroll
+  for (int d = 0; d <= K; ++d) out.lvl[d] = 0;
+  // level 1 -> 2: every root's first segment (picker-1 neighbours), no checks needed
+  uint32_t* cnt = S.cnt;
+  for (int r = tid; r < n0; r += FWG) {
+    const bool ok = S.fwd[r] < S.fwd[r + 1] && (!get_cc || S.parent[r] == target);
+    cnt[r] = ok ? (uint32_t)(S.split[r] - S.fwd[r]) : 0u;
+  }
+  __syncthreads();
+  const int64_t n2 = block_scan_array<FWG>(cnt, n0, H.red64);
+  constexpr bool last = K == 2;
+  if (n2 > 65535 || n2 * (last ? 6 : 4) > qbytes) return out;
+  for (int r = tid; r < n0; r += FWG) {
+    const bool ok = S.fwd[r] < S.fwd[r + 1] && (!get_cc || S.parent[r] == target);
+    if (!ok) continue;
+    uint32_t o = cnt[r];
+    for (int t = S.fwd[r]; t < S.split[r]; ++t, ++o) {
+      const int h = S.dst[t];
+      reinterpret_cast<uint32_t*>(q)[o] = ((uint32_t)r << 16) | (uint32_t)h;
+      if (last) {
+        S.flags[r] = 3;
+        S.flags[h] = 3;
+        reinterpret_cast<uint16_t*>(q + 4 * (int)n2)[o] = 0;
+      }
+    }
+  }
+  __syncthreads();
+  out.lvl[2] = 0;
+  if constexpr (K > 2) {
+    return BfsLevel<K, 2>::run(S, H, q, qbytes, out, n2, tid);
+  } else {
+    out.C = n2;
+    return out;
+  }
+}
+
 // Candidates of a box: the 3x3 cell stencil around its cell in the grid of every HIGHER
 // picker (forward edges only), i.e. up to 3 (K - 1 - p) column ranges of sorted positions.
 struct Stencil {
@@ -925,36 +1072,48 @@ void k_fused(FusedArgs A) {
 
   STOP_AFTER(3);
   STAMP(7);   // CC stats
-  // ---- P4: clique count per picker-0 root, vertex marking, output reservation
+  // ---- P4: k-cliques (level-synchronous BFS into the queue region; per-root DFS counts as the
+  // fallback when a level does not fit), vertex marking, output reservation
   c.set_order = 2 * K < H.nodes;
-  // the clique queue starts right after the E used entries of dst (dst's unused tail and the
-  // cell starts are contiguous: dst immediately precedes the cell starts in the layout)
-  {
-    const int qoff = (L.off_dst + 2 * H.E + 3) & ~3;
-    S.cbuf = reinterpret_cast<uint16_t*>(smem + qoff);
-    c.S.cbuf = S.cbuf;
-    c.cq_cap = (L.off_parent - qoff) / (2 * K + 2);
-    c.cq_ord = S.cbuf + c.cq_cap * K;
-  }
-  c.ccur = &H.ccur;
   const int n0 = c.pp[1];   // roots: picker-0 positions
   const int target = H.target;
-  for (int r = tid; r < n0; r += FWG) {
-    uint32_t cntr = 0;
-    if (S.fwd[r] < S.fwd[r + 1] && (!get_cc || S.parent[r] == (uint32_t)target)) {
-      int mem[K];
-      mem[0] = r;
-      c.count = 0;
-      FLevel<K, 1, false>::run(c, mem);
-      cntr = (uint32_t)c.count;
+  // queue region: after the E used entries of dst through the cell starts (contiguous: dst
+  // immediately precedes the cell starts in the layout)
+  const int qoff = (L.off_dst + 2 * H.E + 15) & ~15;
+  const int qbytes = L.off_parent - qoff;
+  char* const q = smem + qoff;
+  const BfsOut<K> bo = bfs_cliques<K>(S, H, q, qbytes, n0, get_cc, (uint32_t)target, tid);
+  const bool bfs_ok = bo.C >= 0;
+  int64_t C;
+  if (bfs_ok) {
+    C = bo.C;
+    // cliques = level-K tree entries (members by walking parents); their flag words follow
+    c.cq_cap = (int)max(C, (int64_t)1);
+    c.cq_ord = reinterpret_cast<uint16_t*>(q + bo.lvl[K] + 4 * (int)C);
+  } else {
+    S.cbuf = reinterpret_cast<uint16_t*>(smem + qoff);
+    c.cq_cap = 0;   // the DFS only counts; P6 re-walks it chunk by chunk
+    c.ccur = &H.ccur;
+    for (int r = tid; r < n0; r += FWG) {
+      uint32_t cntr = 0;
+      if (S.fwd[r] < S.fwd[r + 1] && (!get_cc || S.parent[r] == (uint32_t)target)) {
+        int mem[K];
+        mem[0] = r;
+        c.count = 0;
+        FLevel<K, 1, false>::run(c, mem);
+        cntr = (uint32_t)c.count;
+      }
+      S.cnt[r] = cntr;
     }
-    S.cnt[r] = cntr;
+    __syncthreads();
+    C = block_scan_array<FWG>(S.cnt, n0, H.red64);
+    if (tid == 0) S.cnt[n0] = (uint32_t)C;
+    c.cq_cap = qbytes / (2 * K + 2);
+    c.cq_ord = S.cbuf + (size_t)c.cq_cap * K;
   }
-  __syncthreads();
-  STAMP(8);   // DFS
-  const int64_t C = block_scan_array<FWG>(S.cnt, n0, H.red64);
+  c.S.cbuf = S.cbuf;
+  STAMP(8);   // cliques
   if (tid == 0) {
-    S.cnt[n0] = (uint32_t)C;
     H.C = C;
     if (C == 0) {
       H.status = RGC_ST_NO_CLIQUES;
@@ -1028,12 +1187,21 @@ void k_fused(FusedArgs A) {
     // kept in the low bits).  Micrographs whose cliques overflowed the queue re-walk the DFS
     // per chunk of <= cq_cap cliques into the same buffer.
     const int64_t Cm = H.C;
-    const bool queued = Cm <= c.cq_cap;
+    // members of chunk slot sl: BFS tree walk, or the re-walk buffer
+    auto clique_members = [&](int64_t sl, int (&mem)[K]) {
+      if (bfs_ok) {
+        BfsLevel<K, K>::prefix(q, bo.lvl, (uint32_t)sl, mem);
+      } else {
+        const uint16_t* sb = S.cbuf + sl * K;
+#pragma unroll
+        for (int i = 0; i < K; ++i) mem[i] = sb[i];
+      }
+    };
     int ci = 0;
     for (int64_t c0 = 0; c0 < Cm; c0 += c.cq_cap, ++ci) {
       const int64_t c1 = min(Cm, c0 + (int64_t)c.cq_cap);
       if (tid == 0) H.tief[(ci + 1) & 1] = 0;   // last read before the previous chunk's end
-      if (!queued) {
+      if (!bfs_ok) {
         c.c0 = c0;
         c.c1 = c1;
         for (int r = tid; r < n0; r += FWG) {
@@ -1049,10 +1217,8 @@ void k_fused(FusedArgs A) {
       bool any = false;
       for (int64_t sl = tid; sl < c1 - c0; sl += FWG) {
         int mem[K];
-        const uint16_t* sb = S.cbuf + sl * K;
-#pragma unroll
-        for (int i = 0; i < K; ++i) mem[i] = sb[i];
-        const int64_t j = queued ? S.cnt[mem[0]] + c.cq_ord[sl] : c0 + sl;
+        clique_members(sl, mem);
+        const int64_t j = c0 + sl;
         if (fused_epilogue_main<K, W>(c, H.base + j, mem)) {
           c.cq_ord[sl] |= 0x8000;
           any = true;
@@ -1065,10 +1231,8 @@ void k_fused(FusedArgs A) {
           const uint32_t o = c.cq_ord[sl];
           if (!(o & 0x8000)) continue;
           int mem[K];
-          const uint16_t* sb = S.cbuf + sl * K;
-#pragma unroll
-          for (int i = 0; i < K; ++i) mem[i] = sb[i];
-          const int64_t j = queued ? S.cnt[mem[0]] + (o & 0x7FFF) : c0 + sl;
+          clique_members(sl, mem);
+          const int64_t j = c0 + sl;
           fused_epilogue_order<K, W>(c, H.base + j, mem);
         }
       }
