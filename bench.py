@@ -120,12 +120,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RGC_BENCH_DEVICE / RGC_DIST_BACKEND: test hooks (two ranks on one GPU over gloo);
+    # the driver's runs use one GPU per rank over RCCL ("nccl")
+    local = int(os.environ.get("RGC_BENCH_DEVICE", local))
+    backend = os.environ.get("RGC_DIST_BACKEND", "nccl")
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
+    cdev = dev if backend == "nccl" else torch.device("cpu")   # collective tensors
 
     from repic_amd import _lib, synth
     from repic_amd.pipeline import Batch
@@ -138,7 +146,7 @@ def main():
     t_gen = time.time() - t_gen
     # the one exchange of the sharded path: global box-id offsets
     if dist is not None:
-        tot = torch.tensor([batch.n_boxes], dtype=torch.int64, device=dev)
+        tot = torch.tensor([batch.n_boxes], dtype=torch.int64, device=cdev)
         allt = [torch.zeros_like(tot) for _ in range(world)]
         dist.all_gather(allt, tot)
         id_off = int(sum(int(t.item()) for t in allt[:rank]))
@@ -175,11 +183,11 @@ def main():
     N, E, C = int(r.n_boxes), int(r.n_edges), int(r.n_cliques)
     V = int(r.n_vert.sum())
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         # single end-of-run reduction of node-level counts over RCCL/xGMI
-        cnt = torch.tensor([n_mg, E, C], dtype=torch.int64, device=dev)
+        cnt = torch.tensor([n_mg, E, C], dtype=torch.int64, device=cdev)
         dist.all_reduce(cnt)
         tot_mg, tot_e, tot_c = (int(v) for v in cnt.tolist())
     else:
@@ -207,6 +215,7 @@ def main():
                    "boxes_per_gpu": N, "edges_per_gpu": E, "cliques_per_gpu": C,
                    "parallelism": f"dp{world} (micrograph shards)"},
         "edges_per_sec": tot_e * steps / elapsed,
+        "totals": {"micrographs": tot_mg, "edges": tot_e, "cliques": tot_c},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": traffic_src,

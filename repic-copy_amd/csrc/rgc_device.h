@@ -126,6 +126,13 @@ __device__ __forceinline__ int64_t block_scan_u16(uint16_t* a, int n, int64_t* l
 }
 
 // ----------------------------------------------------------------------------- arithmetic
+// overlap area of two boxes, reference op order (get_cliques.py:42-44), no FMA.
+__host__ __device__ __forceinline__ double overlap(double x, double y, double a, double b, double B) {
+  const double xo = fmax((fmin(x, a) + B) - fmax(x, a), 0.0);
+  const double yo = fmax((fmin(y, b) + B) - fmax(y, b), 0.0);
+  return xo * yo;
+}
+
 // reference calc_jaccard (get_cliques.py:40-46), same f64 op order, no FMA.
 __host__ __device__ __forceinline__ double jaccard(double x, double y, double a, double b, double B,
                                           double two_b2) {
@@ -146,6 +153,18 @@ __device__ __forceinline__ bool is_edge(double xa, double ya, double xb, double 
 // numpy median (numpy/lib/_function_base_impl.py _median): middle value, or the mean of the
 // two middle values ((a + b) / 2) for even n; NaN if any value is NaN.  Sorting network on a
 // register array (fully unrolled: no scratch).
+template <int N>
+__host__ __device__ __forceinline__ void sort_n(double (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < N - 1 - i; ++j) {
+      const double a = v[j], b = v[j + 1];
+      v[j] = fmin(a, b);
+      v[j + 1] = fmax(a, b);
+    }
+}
+
 template <int N>
 __host__ __device__ __forceinline__ double median_n(double (&v)[N]) {
   bool nan = false;

@@ -278,10 +278,11 @@ __device__ __forceinline__ uint64_t ins_key(const FCtx<K>& c, int u) {
 template <int K, bool W>
 __device__ __forceinline__ bool fused_epilogue_main(const FCtx<K>& c, int64_t j,
                                                     const int (&mem)[K]) {
-  double ji[K][K], xs[K], ys[K];
-  int li[K];   // local (file-order) indices: id order
+  constexpr int NE = K * (K - 1) / 2;
+  double I[NE];   // overlaps of the member pairs (a < b) in reference op order
+  int li[K];      // local (file-order) indices: id order
   {
-    double s[K];
+    double s[K], xs[K], ys[K];
     int r[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
@@ -308,22 +309,68 @@ __device__ __forceinline__ bool fused_epilogue_main(const FCtx<K>& c, int64_t j,
       }
 #pragma unroll
     for (int i = 0; i < K; ++i) c.rows[j * K + i] = r[i];
+    {
+      int t = 0;
 #pragma unroll
-    for (int a = 0; a < K; ++a)
+      for (int a = 0; a < K; ++a)
 #pragma unroll
-      for (int b = a + 1; b < K; ++b) ji[a][b] = jaccard(xs[a], ys[a], xs[b], ys[b], c.B, c.two_b2);
-    float w, conf;
-    epi_weights<K>(ji, s, &w, &conf);
-    c.w[j] = w;
-    c.conf[j] = conf;
+        for (int b = a + 1; b < K; ++b) I[t++] = overlap(xs[a], ys[a], xs[b], ys[b], c.B);
+    }
+    // conf = f32(median score); w = f32(f64(conf) * median JI) where median JI = JI of the
+    // median overlap (JI = I / (2 B^2 - I) is non-decreasing in I, so sorting by I sorts the
+    // JIs): one or two reference divisions instead of one per pair
+    const double cf = median_n<K>(s);
+    double Is[NE];
+#pragma unroll
+    for (int t = 0; t < NE; ++t) Is[t] = I[t];
+    double med;
+    if (NE & 1) {
+      med = median_n<NE>(Is);   // sorted copy's middle element
+      med = med / (c.two_b2 - med);
+    } else {
+      bool nan = false;
+#pragma unroll
+      for (int t = 0; t < NE; ++t) nan |= isnan(Is[t]);
+      sort_n<NE>(Is);
+      const double a = Is[NE / 2 - 1], b = Is[NE / 2];
+      med = nan ? NAN : ((a / (c.two_b2 - a)) + (b / (c.two_b2 - b))) / 2.0;
+    }
+    const float conf32 = (float)cf;
+    c.w[j] = (float)((double)conf32 * med);
+    c.conf[j] = conf32;
   }
   if (c.flags & (2 | 32)) {
 #pragma unroll
     for (int i = 0; i < K; ++i) c.members[j * K + i] = c.b0 + li[i];
   }
-  uint32_t top;
-  const int arg = epi_degree_max<K>(ji, &top);
-  if ((top & (top - 1)) != 0 || (c.flags & 2)) return true;
+  if (c.flags & 2) return true;
+  // weighted degrees from f32 JIs (error < 2e-6 absolute per sum): a clear maximum is the
+  // reference's; anything within 1e-5 goes to the exact f64 pass (ties included)
+  float deg[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) deg[i] = 0.0f;
+  {
+    int t = 0;
+#pragma unroll
+    for (int a = 0; a < K; ++a)
+#pragma unroll
+      for (int b = a + 1; b < K; ++b) {
+        const float jf = (float)I[t] / (float)(c.two_b2 - I[t]);
+        deg[a] += jf;
+        deg[b] += jf;
+        ++t;
+      }
+  }
+  float d1 = deg[0], d2 = -INFINITY;
+  int arg = 0;
+#pragma unroll
+  for (int i = 1; i < K; ++i) {
+    const float d = deg[i];
+    d2 = d > d1 ? d1 : fmaxf(d2, d);
+    arg = d > d1 ? i : arg;
+    d1 = fmaxf(d1, d);
+  }
+  if (!(d1 - d2 > 1e-5f)) return true;
   int cons = li[0];
 #pragma unroll
   for (int i = 1; i < K; ++i) cons = (arg == i) ? li[i] : cons;
@@ -349,25 +396,28 @@ __device__ __forceinline__ void fused_epilogue_order(const FCtx<K>& c, int64_t j
     li[i] = c.S.citems[mem[i]];
     ids[i] = c.idb + li[i];
   }
-  if (!c.set_order) {
-    for (int i = 0; i < K; ++i) ins[i] = ins_key<K>(c, mem[i]);
-  }
 #pragma unroll
   for (int a = 0; a < K; ++a)
 #pragma unroll
     for (int b = a + 1; b < K; ++b) ji[a][b] = jaccard(xs[a], ys[a], xs[b], ys[b], c.B, c.two_b2);
+  if (!c.set_order) {
+    for (int i = 0; i < K; ++i) ins[i] = ins_key<K>(c, mem[i]);
+  }
   uint32_t top;
   int arg = epi_degree_max<K>(ji, &top);
-  const uint32_t ord = node_order<K>(li, xs, ys, ids, c.set_order, ins);
-  if ((top & (top - 1)) != 0) arg = epi_tie_arg<K>(top, ord);
+  const bool tie = (top & (top - 1)) != 0;
+  if (tie || (c.flags & 2)) {
+    const uint32_t ord = node_order<K>(li, xs, ys, ids, c.set_order, ins);
+    if (tie) arg = epi_tie_arg<K>(top, ord);
+    if (c.flags & 2) {
+#pragma unroll
+      for (int i = 0; i < K; ++i) c.order[j * K + i] = (uint8_t)((ord >> (4 * i)) & 15);
+    }
+  }
   int cons = li[0];
 #pragma unroll
   for (int i = 1; i < K; ++i) cons = (arg == i) ? li[i] : cons;
   c.consensus[j] = c.b0 + cons;
-  if (c.flags & 2) {
-#pragma unroll
-    for (int i = 0; i < K; ++i) c.order[j * K + i] = (uint8_t)((ord >> (4 * i)) & 15);
-  }
 }
 
 // Static-recursion DFS: level D picks the picker-D member among the forward neighbours of

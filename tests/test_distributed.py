@@ -130,3 +130,30 @@ def test_cli_two_ranks_match_golden(name, tmp_path):
         assert excs == [None, None]
     mgs, arrays = read_outputs(os.path.join(str(tmp_path), "out"), meta)
     assert_matches_golden(meta, data, mgs, arrays)
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_one_gpu():
+    """bench.py's sharded path (id-offset all_gather, max-over-ranks timing, counter
+    all_reduce) with two ranks on cuda:0 over gloo: the totals equal one rank's run over the
+    union of the shards."""
+    def run(world, n_mg):
+        port = _free_port()
+        procs = []
+        for r in range(world):
+            env = dict(os.environ, WORLD_SIZE=str(world), RANK=str(r), LOCAL_RANK=str(r),
+                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RGC_BENCH_DEVICE="0",
+                       RGC_DIST_BACKEND="gloo")
+            procs.append(subprocess.Popen(
+                [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--n_mg",
+                 str(n_mg), "--steps", "2", "--warmup", "1", "--no-cpu-baseline"],
+                env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+        outs = [p.communicate(timeout=240) for p in procs]
+        for p, (o, e) in zip(procs, outs):
+            assert p.returncode == 0, e[-3000:]
+        return json.loads(outs[0][0].strip().splitlines()[-1])
+    two = run(2, 60)
+    one = run(1, 120)
+    assert two["n_gpus"] == 2 and two["value"] > 0 and two["scaling"] == "weak"
+    assert two["totals"] == one["totals"]
+    assert two["totals"]["micrographs"] == 120
