@@ -211,29 +211,35 @@ class Context:
 
 
 class Result:
-    """Host view of one rgc_run.  Per-clique arrays are numpy views of pinned host memory
-    (F_HOST_OUTPUTS) or raw device pointers otherwise."""
+    """Host view of one rgc_run.  Per-micrograph and per-clique arrays are numpy views of
+    context-owned pinned memory (per-clique arrays: device pointers without F_HOST_OUTPUTS);
+    like the C-ABI outputs they stay valid until the next ``run`` on the context."""
+
+    _PER_MG = {"status": ("status", np.int32), "cc_max": ("cc_max", np.int32),
+               "cc_cnt": ("cc_cnt", np.int32), "n_nodes": ("n_nodes", np.int32),
+               "n_vert": ("n_vert", np.int32), "n_edges_mg": ("n_edges_mg", np.int64),
+               "clique_base": ("clique_base", np.int64), "clique_cnt": ("clique_cnt", np.int64)}
+
+    def __getattr__(self, name):
+        # per-micrograph arrays are built on first use (views, no copy)
+        spec = Result._PER_MG.get(name)
+        if spec is None:
+            raise AttributeError(name)
+        field, dt = spec
+        dt = np.dtype(dt)
+        p = getattr(self._bo, field)
+        if not self.n_mg or not p:
+            v = np.zeros(0, dt)
+        else:
+            addr = C.cast(p, C.c_void_p).value
+            v = np.frombuffer((C.c_char * (self.n_mg * dt.itemsize)).from_address(addr), dt)
+        setattr(self, name, v)
+        return v
 
     def __init__(self, bo: BatchOut, n_mg: int, k: int, flags: int):
+        self._bo = bo
         self.n_mg, self.k = n_mg, k
         self.n_boxes, self.n_edges, self.n_cliques = bo.n_boxes, bo.n_edges, bo.n_cliques
-
-        def a(p, n, dt):
-            """copy of n library-owned values (the library reuses the memory next run)"""
-            dt = np.dtype(dt)
-            if not n:
-                return np.zeros(0, dt)
-            addr = C.cast(p, C.c_void_p).value
-            return np.frombuffer((C.c_char * (n * dt.itemsize)).from_address(addr), dt).copy()
-
-        self.status = a(bo.status, n_mg, np.int32)
-        self.cc_max = a(bo.cc_max, n_mg, np.int32)
-        self.cc_cnt = a(bo.cc_cnt, n_mg, np.int32)
-        self.n_nodes = a(bo.n_nodes, n_mg, np.int32)
-        self.n_vert = a(bo.n_vert, n_mg, np.int32)
-        self.n_edges_mg = a(bo.n_edges_mg, n_mg, np.int64)
-        self.clique_base = a(bo.clique_base, n_mg, np.int64)
-        self.clique_cnt = a(bo.clique_cnt, n_mg, np.int64)
         C_ = int(self.n_cliques)
         if flags & F_HOST_OUTPUTS:
             def h(p, ct, n):
