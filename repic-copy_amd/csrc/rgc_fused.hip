@@ -159,6 +159,16 @@ __device__ __forceinline__ uint32_t uf_find_lds(uint32_t* parent, uint32_t x) {
     x = gp;
   }
 }
+// lock-free union (link the larger root under the smaller), workgroup-scope LDS atomics
+__device__ __forceinline__ void uf_union_lds(uint32_t* parent, uint32_t a, uint32_t b) {
+  for (;;) {
+    a = uf_find_lds(parent, a);
+    b = uf_find_lds(parent, b);
+    if (a == b) return;
+    if (a < b) { const uint32_t t = a; a = b; b = t; }
+    if (atomicCAS(&parent[a], a, b) == a) return;
+  }
+}
 
 template <int K>
 __device__ __forceinline__ int picker_of(const int (&pb)[K + 1], int i) {
@@ -1020,7 +1030,11 @@ void k_fused(FusedArgs A) {
   __syncthreads();
   STAMP(4);   // scan
   if (H.status == 0) {
-    // fill + sort each list, then union its edges (lock-free union-find, P3's first half)
+    // fill each list (already sorted: position order) and record each edge's source in dst's
+    // unused tail when it has room; then union the edges one thread per edge (lock-free
+    // union-find, balanced across lanes whatever the degrees).  Without room: union per box.
+    const bool src_ok = 2 * E <= A.ecap;
+    uint16_t* esrc = S.dst + E;
     for (int ts = tid; ts < n; ts += FWG) {
       const int i = ts;
       const int base = S.fwd[i], cnt = (int)S.fwd[i + 1] - base;
@@ -1030,23 +1044,24 @@ void k_fused(FusedArgs A) {
       uint16_t* d = S.dst + base;
       pairs_fill<K, W>(st, S, G, S.cnt[ts], d, cnt, B, two_b2, i_lo, i_hi);
       S.flags[i] = 1;
-#ifdef RGC_X_NOUNION
-      continue;   // timing experiment only (wrong CC outputs)
-#endif
-      for (int e = 0; e < cnt; ++e) {
-        const uint32_t h = d[e];
-        S.flags[h] = 1;
-        uint32_t a = i, b = h;
-        for (;;) {
-          a = uf_find_lds(S.parent, a);
-          b = uf_find_lds(S.parent, b);
-          if (a == b) break;
-          if (a < b) { const uint32_t t = a; a = b; b = t; }
-          if (atomicCAS(&S.parent[a], a, b) == a) break;
+      if (src_ok) {
+        for (int e = 0; e < cnt; ++e) esrc[base + e] = (uint16_t)i;
+      } else {
+        for (int e = 0; e < cnt; ++e) {
+          S.flags[d[e]] = 1;
+          uf_union_lds(S.parent, (uint32_t)i, (uint32_t)d[e]);
         }
       }
     }
     __syncthreads();
+    if (src_ok) {
+      for (int e = tid; e < E; e += FWG) {
+        const uint32_t h = S.dst[e];
+        S.flags[h] = 1;
+        uf_union_lds(S.parent, esrc[e], h);
+      }
+      __syncthreads();
+    }
     STAMP(5);   // fill + sort
   }
   if (H.status != 0) {
