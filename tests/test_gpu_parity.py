@@ -187,3 +187,25 @@ def test_gpu_full_c2_properties():
     # weight = f32(f64(conf) * median JI) >= 0.3 * conf; conf is a member's score median
     assert (r.w > 0).all() and (r.w <= r.conf).all()
     ctx.close()
+
+
+def test_gpu_mixed_batch_routes():
+    """One batch whose micrographs take every route: f32-layout fused pass, f64 relaunch
+    (coordinates not exact in f32), large-LDS relaunch (dense clusters), BFS overflow into
+    the DFS re-walk, and the multi-kernel path (more boxes than the fused kernel's LDS)."""
+    from repic_amd import synth
+    cfg = synth.SynthConfig(**synth.CONFIGS["C2"], seed=11)
+    base = synth.batch(cfg, 6)
+    mgs = [base[0], base[1]]
+    # non-f32-exact coordinates
+    mgs.append([(x + 0.001, y - 0.0005, s) for (x, y, s) in base[2]])
+    # dense near-duplicate clusters (many more cliques than boxes)
+    mgs.append(_dense_clusters(3, 10, 4, seed=7))
+    mgs.append(base[3])
+    # a large micrograph: too many boxes for the fused kernel
+    big = synth.SynthConfig(k=3, n_true=1500, box=60, width=4096, height=4096, keep=0.9,
+                            jit=0.08, fp=0.1, seed=12)
+    mgs.append(synth.batch(big, 1)[0])
+    mgs.append(base[4])
+    _check_vs_oracle(mgs, 3, 100)
+    _check_vs_oracle(mgs, 3, 100, get_cc=True)
