@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RGC_ABI_VERSION 1
+#define RGC_ABI_VERSION 2
 
 /* flags for rgc_batch_in.flags */
 #define RGC_F_GET_CC         1u  /* --get_cc   (get_cliques.py:151-156) */
@@ -37,6 +37,9 @@ extern "C" {
 #define RGC_F_MEMBERS       32u  /* also return the k member boxes of every clique */
 #define RGC_F_NO_FUSED      64u  /* route every micrograph through the multi-kernel path
                                     (testing / comparison; outputs are identical) */
+#define RGC_F_DEVICE_META  128u  /* dev_box_off / dev_id_base hold HBM-resident copies of
+                                    box_off (as int32) and id_base: no offset upload per run
+                                    (the host arrays are still read for launch planning) */
 
 /* per-micrograph status (rgc_batch_out.status) */
 #define RGC_OK          0   /* outputs written as in get_cliques.py:215-229 */
@@ -57,6 +60,8 @@ typedef struct rgc_batch_in {
   const double* x;         /* [N] box x (common.py:87), host or device per flags */
   const double* y;         /* [N] box y */
   const double* score;     /* [N] score, sigmoid already applied on host (common.py:92-94) */
+  const int32_t* dev_box_off;  /* DEVICE [n_mg*k+1], int32 copy of box_off (RGC_F_DEVICE_META) */
+  const int64_t* dev_id_base;  /* DEVICE [n_mg], copy of id_base (RGC_F_DEVICE_META) */
 } rgc_batch_in;
 
 typedef struct rgc_batch_out {

@@ -151,6 +151,7 @@ struct rgc_ctx {
   std::vector<float> times;
   std::vector<const char*> time_names;
   int64_t cap_cliques = 0;   // capacity of the per-clique output arrays
+  void* cursor_zeroed = nullptr;   // fused cursor already cleared on the stream for next run
   std::vector<uint64_t> stamps;   // diagnostic build only
 };
 
@@ -398,8 +399,11 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   c->n_ev = 0;
 
   // per-micrograph outputs: pinned SoA block, filled by one copy of the device mirror
-  TRY(ensure_host(c, H_MGOUT, mgout_bytes(n_mg)));
-  TRY(ensure_dev(c, D_MGOUT, mgout_bytes(n_mg)));
+  // the fused kernels' reservation cursor (16 B) sits right after the per-micrograph block,
+  // so one copy returns both
+  const size_t cur_off = (mgout_bytes(n_mg) + 15) & ~(size_t)15;
+  TRY(ensure_host(c, H_MGOUT, cur_off + 16));
+  TRY(ensure_dev(c, D_MGOUT, cur_off + 16));
   const MgOut ho = mgout_bind(H<void>(c, H_MGOUT), n_mg);
   const MgOut dout = mgout_bind(D<void>(c, D_MGOUT), n_mg);
   std::memset(out, 0, sizeof(*out));
@@ -430,16 +434,28 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   int64_t* f_id = reinterpret_cast<int64_t*>(
       (reinterpret_cast<uintptr_t>(f_bo + nbo) + 7) & ~(uintptr_t)7);
   int32_t* f_ml = reinterpret_cast<int32_t*>(f_id + n_mg);
-  for (size_t i = 0; i < nbo; ++i) f_bo[i] = (int32_t)in->box_off[i];
-  std::memcpy(f_id, in->id_base, n_mg * 8);
-  TRY(ensure_dev(c, D_FBOXOFF, nbo * 4));
-  TRY(ensure_dev(c, D_FIDBASE, n_mg * 8));
+  // per-micrograph offsets on the device: the caller's HBM-resident copies, or an upload
+  const bool dev_meta = (flags & RGC_F_DEVICE_META) != 0;
+  if (dev_meta && (!in->dev_box_off || !in->dev_id_base))
+    return fail("RGC_F_DEVICE_META needs dev_box_off and dev_id_base");
   TRY(ensure_dev(c, D_MGLIST, 3 * (size_t)n_mg * 4 + 4));
-  TRY(ensure_dev(c, D_CURSOR, 16));
-  TRY(ensure_host(c, H_TOTAL, 16));
-  TRY(mark(c, "h2d_meta"));
-  HIPCHK(hipMemcpyAsync(D<void>(c, D_FBOXOFF), f_bo, nbo * 4, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(D<void>(c, D_FIDBASE), f_id, n_mg * 8, hipMemcpyHostToDevice, s));
+  unsigned long long* d_cur = reinterpret_cast<unsigned long long*>(
+      static_cast<char*>(D<void>(c, D_MGOUT)) + cur_off);
+  const unsigned long long* h_cur = reinterpret_cast<const unsigned long long*>(
+      static_cast<const char*>(H<void>(c, H_MGOUT)) + cur_off);
+  const int32_t* d_bo = in->dev_box_off;
+  const int64_t* d_id = in->dev_id_base;
+  if (!dev_meta) {
+    for (size_t i = 0; i < nbo; ++i) f_bo[i] = (int32_t)in->box_off[i];
+    std::memcpy(f_id, in->id_base, n_mg * 8);
+    TRY(ensure_dev(c, D_FBOXOFF, nbo * 4));
+    TRY(ensure_dev(c, D_FIDBASE, n_mg * 8));
+    TRY(mark(c, "h2d_meta"));
+    HIPCHK(hipMemcpyAsync(D<void>(c, D_FBOXOFF), f_bo, nbo * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(D<void>(c, D_FIDBASE), f_id, n_mg * 8, hipMemcpyHostToDevice, s));
+    d_bo = D<int32_t>(c, D_FBOXOFF);
+    d_id = D<int64_t>(c, D_FIDBASE);
+  }
   if (!(flags & RGC_F_DEVICE_INPUTS)) {
     TRY(ensure_dev(c, D_X, N * 8));
     TRY(ensure_dev(c, D_Y, N * 8));
@@ -496,13 +512,16 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
     if (c->cap_cliques < 4096) c->cap_cliques = std::max<int64_t>(4096, N);
     for (int attempt = 0; attempt < 2; ++attempt) {
       TRY(ensure_outputs(c, c->cap_cliques, 0, k, want_members, multi != 0));
-      HIPCHK(hipMemsetAsync(D<void>(c, D_CURSOR), 0, 16, s));
+      // the previous run cleared the cursor after its last read (off this run's critical
+      // path); otherwise (first run, moved buffer, regrow attempt) clear it here
+      if (attempt > 0 || c->cursor_zeroed != d_cur) HIPCHK(hipMemsetAsync(d_cur, 0, 16, s));
+      c->cursor_zeroed = nullptr;
       FusedArgs A;
       A.k = k; A.flags = get_cc | (multi << 1) | (want_members ? 32 : 0);
       A.B = B; A.two_b2 = two_b2;
-      A.box_off = D<int32_t>(c, D_FBOXOFF); A.id_base = D<int64_t>(c, D_FIDBASE);
+      A.box_off = d_bo; A.id_base = d_id;
       A.x = x; A.y = y; A.score = sc; A.o = dout;
-      A.cursor = D<unsigned long long>(c, D_CURSOR); A.cap = c->cap_cliques;
+      A.cursor = d_cur; A.cap = c->cap_cliques;
       A.rows = D<int32_t>(c, D_ROWS); A.w = D<float>(c, D_W); A.conf = D<float>(c, D_CONF);
       A.consensus = D<int32_t>(c, D_CONS);
       A.members = want_members ? D<int32_t>(c, D_MEMBERS) : nullptr;
@@ -569,9 +588,8 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
                         (le > 0 ? hipGetErrorString((hipError_t)le) : "unsupported k"));
         }
         TRY(mark(c, "d2h_stats"));
-        HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOUT), D<void>(c, D_MGOUT), mgout_bytes(n_mg),
+        HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOUT), D<void>(c, D_MGOUT), cur_off + 16,
                               hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(H<void>(c, H_TOTAL), D<void>(c, D_CURSOR), 16, hipMemcpyDeviceToHost, s));
         HIPCHK(hipGetLastError());
         HIPCHK(hipStreamSynchronize(s));
         const int32_t* fst = ho.status;
@@ -590,7 +608,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
         }
         for (int32_t m : left) todo.push_back(m);
       }
-      fused_total = (int64_t)H<unsigned long long>(c, H_TOTAL)[0];
+      fused_total = (int64_t)h_cur[0];
 #ifdef RGC_STAMPS
       const size_t n0w = all0 ? (size_t)n_mg : todo0.size();   // pass 0's workgroups
       c->stamps.resize(n0w * 16);
@@ -604,7 +622,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
       c->cap_cliques = fused_total + fused_total / 8 + 1024;   // grow and re-run once
       c->n_ev = 0;
     }
-    E_total = (int64_t)H<unsigned long long>(c, H_TOTAL)[1];   // finished micrographs
+    E_total = (int64_t)h_cur[1];   // finished micrographs
   }
 
   int64_t C_total = fused_total;
@@ -633,7 +651,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
     HIPCHK(hipMemcpy(D<void>(c, D_SUBMG), deferred.data(), ns * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(D<void>(c, D_BOXOFF), sbo32.data(), sbo32.size() * 4, hipMemcpyHostToDevice));
     TRY(mark(c, "k_gather"));
-    launch_gather(s, ns, k, D<int32_t>(c, D_SUBMG), D<int32_t>(c, D_FBOXOFF), D<int32_t>(c, D_BOXOFF),
+    launch_gather(s, ns, k, D<int32_t>(c, D_SUBMG), d_bo, D<int32_t>(c, D_BOXOFF),
                   x, y, sc, D<double>(c, D_SUBX), D<double>(c, D_SUBY), D<double>(c, D_SUBS),
                   D<int32_t>(c, D_ORIG));
     HIPCHK(hipStreamSynchronize(s));
@@ -702,6 +720,11 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   TRY(mark(c, "end"));
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
+  if (all0 || !todo0.empty()) {
+    // clear the cursor for the next run now, while the host is busy elsewhere
+    HIPCHK(hipMemsetAsync(d_cur, 0, 16, s));
+    c->cursor_zeroed = d_cur;
+  }
 
 
   if (c->timing) {

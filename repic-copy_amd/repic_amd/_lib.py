@@ -23,7 +23,7 @@ if not os.path.exists(LIB_PATH):
 lib = C.CDLL(LIB_PATH)
 
 F_GET_CC, F_MULTI_OUT, F_DEVICE_INPUTS, F_HOST_OUTPUTS, F_TIMING = 1, 2, 4, 8, 16
-F_MEMBERS, F_NO_FUSED = 32, 64
+F_MEMBERS, F_NO_FUSED, F_DEVICE_META = 32, 64, 128
 OK, NO_EDGES, NO_CLIQUES = 0, 1, 2
 PARSE_OK, PARSE_INDEX, PARSE_VALUE, PARSE_ASSERT, PARSE_FALLBACK, PARSE_OSERROR = range(6)
 MAX_K = 8
@@ -38,7 +38,8 @@ _u8p = C.POINTER(C.c_uint8)
 class BatchIn(C.Structure):
     _fields_ = [("n_mg", C.c_int32), ("k", C.c_int32), ("box_size", C.c_int64),
                 ("flags", C.c_uint32), ("box_off", _i64p), ("id_base", _i64p),
-                ("x", C.c_void_p), ("y", C.c_void_p), ("score", C.c_void_p)]
+                ("x", C.c_void_p), ("y", C.c_void_p), ("score", C.c_void_p),
+                ("dev_box_off", C.c_void_p), ("dev_id_base", C.c_void_p)]
 
 
 class BatchOut(C.Structure):
@@ -178,11 +179,14 @@ class Context:
         except Exception:  # noqa: BLE001
             pass
 
-    def run(self, n_mg, k, box_size, box_off, id_base, x, y, score, flags=F_HOST_OUTPUTS):
+    def run(self, n_mg, k, box_size, box_off, id_base, x, y, score, flags=F_HOST_OUTPUTS,
+            dev_meta=None):
         """Run the batched pipeline.  ``box_off``/``id_base`` are host int64 arrays;
         ``x``/``y``/``score`` are host float64 arrays, or device pointers (ints) with
-        ``F_DEVICE_INPUTS``.  Returns a :class:`Result` (views into context-owned memory
-        that stay valid until the next ``run``)."""
+        ``F_DEVICE_INPUTS``.  ``dev_meta`` = (device pointer of box_off as int32, device
+        pointer of id_base) sets ``F_DEVICE_META``: the offsets are not uploaded per run.
+        Returns a :class:`Result` (views into context-owned memory that stay valid until the
+        next ``run``)."""
         box_off = np.ascontiguousarray(box_off, dtype=np.int64)
         id_base = np.ascontiguousarray(id_base, dtype=np.int64)
         assert box_off.shape == (n_mg * k + 1,) and id_base.shape == (n_mg,)
@@ -195,8 +199,12 @@ class Context:
             assert x.shape == y.shape == score.shape == (n,)
             keep += [x, y, score]
             px, py, ps = (C.c_void_p(v.ctypes.data) for v in (x, y, score))
+        dbo = did = None
+        if dev_meta is not None:
+            flags |= F_DEVICE_META
+            dbo, did = (C.c_void_p(int(v)) for v in dev_meta)
         bi = BatchIn(n_mg, k, int(box_size), flags, box_off.ctypes.data_as(_i64p),
-                     id_base.ctypes.data_as(_i64p), px, py, ps)
+                     id_base.ctypes.data_as(_i64p), px, py, ps, dbo, did)
         bo = BatchOut()
         _check(lib.rgc_run(self._p, C.byref(bi), C.byref(bo)))
         del keep

@@ -209,3 +209,71 @@ def test_gpu_mixed_batch_routes():
     mgs.append(base[4])
     _check_vs_oracle(mgs, 3, 100)
     _check_vs_oracle(mgs, 3, 100, get_cc=True)
+
+
+def test_gpu_device_resident_inputs_and_offsets():
+    """F_DEVICE_INPUTS + F_DEVICE_META (the bench's HBM-resident handoff: coordinates, scores,
+    box offsets and id bases already on the device) give the same outputs as host inputs, on
+    a batch that takes every route (fused f32/f64, multi-kernel gather of the big micrograph).
+    Runs in a child process: torch's bundled HIP runtime must initialise before the library's
+    (as in bench.py), and this test process already created library contexts."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join(
+        [root, os.path.join(root, "repic-copy_amd"), here, os.environ.get("PYTHONPATH", "")]))
+    r = subprocess.run([sys.executable, "-c",
+                        "import test_gpu_parity as t; t._device_meta_check(); print('OK')"],
+                       env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout + r.stderr
+
+
+def _device_meta_check():
+    import torch
+    torch.cuda.init()   # torch's HIP runtime first (bench.py order)
+
+    from repic_amd import _lib, synth
+    from repic_amd.pipeline import Batch
+    cfg = synth.SynthConfig(**synth.CONFIGS["C2"], seed=13)
+    base = synth.batch(cfg, 4)
+    big = synth.SynthConfig(k=3, n_true=1500, box=60, width=4096, height=4096, keep=0.9,
+                            jit=0.08, fp=0.1, seed=14)
+    mgs = [base[0], [(x + 0.001, y, s) for (x, y, s) in base[1]], _dense_clusters(3, 10, 4, 9),
+           synth.batch(big, 1)[0], base[2], base[3]]
+    batch = Batch.pack(3, 100, mgs)
+    fl = _lib.F_HOST_OUTPUTS | _lib.F_MEMBERS
+    ctx = _lib.Context(0)
+    a = ctx.run(batch.n_mg, 3, 100, batch.box_off, batch.id_base, batch.x, batch.y,
+                batch.score, fl)
+    per_mg = ("status", "cc_max", "cc_cnt", "n_vert", "clique_cnt")
+    per_cl = ("rows", "w", "conf", "consensus", "members")
+
+    def snap(r):
+        # micrograph ranges are reserved atomically (their order varies); content per range
+        # is deterministic
+        d = {f: np.array(getattr(r, f)) for f in per_mg}
+        for f in per_cl:
+            v = np.asarray(getattr(r, f))
+            d[f] = [v[int(b0):int(b0) + int(n)].copy()
+                    for b0, n in zip(r.clique_base, r.clique_cnt)]
+        return d
+
+    ref = snap(a)
+    dev = torch.device("cuda", 0)
+    dx, dy, ds = (torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+                  for v in (batch.x, batch.y, batch.score))
+    dbo = torch.from_numpy(batch.box_off.astype(np.int32)).to(dev)
+    did = torch.from_numpy(np.ascontiguousarray(batch.id_base, dtype=np.int64)).to(dev)
+    torch.cuda.synchronize()
+    b = ctx.run(batch.n_mg, 3, 100, batch.box_off, batch.id_base, dx.data_ptr(),
+                dy.data_ptr(), ds.data_ptr(), fl | _lib.F_DEVICE_INPUTS,
+                dev_meta=(dbo.data_ptr(), did.data_ptr()))
+    assert (a.n_edges, a.n_cliques) == (b.n_edges, b.n_cliques)
+    got = snap(b)
+    for f in per_mg:
+        assert np.array_equal(ref[f], got[f]), f
+    for f in per_cl:
+        assert all(np.array_equal(u, v) for u, v in zip(ref[f], got[f])), f
+    assert sum(len(v) for v in got["w"]) == int(b.n_cliques)
+    ctx.close()
