@@ -1183,9 +1183,13 @@ void k_fused(FusedArgs A) {
     if (C == 0) {
       H.status = RGC_ST_NO_CLIQUES;
     } else {
-      const unsigned long long base = atomicAdd(A.cursor, (unsigned long long)C);
-      H.base = (int64_t)base;
-      if ((int64_t)base + C > A.cap) H.status = RGC_ST_OVERFLOW;
+      if (C > 0x7fffffff) {
+        H.status = RGC_ST_DEFER;   // P6 indexes a micrograph's cliques in 32 bits
+      } else {
+        const unsigned long long base = atomicAdd(A.cursor, (unsigned long long)C);
+        H.base = (int64_t)base;
+        if ((int64_t)base + C > A.cap) H.status = RGC_ST_OVERFLOW;
+      }
     }
   }
   __syncthreads();
@@ -1251,9 +1255,14 @@ void k_fused(FusedArgs A) {
     // the cliques it flagged (bit 15 of the slot's ordinal word; the slot's output index is
     // kept in the low bits).  Micrographs whose cliques overflowed the queue re-walk the DFS
     // per chunk of <= cq_cap cliques into the same buffer.
-    const int64_t Cm = H.C;
+    // chunk bounds and the output base are wave-uniform and 32-bit (C < 2^31, checked at the
+    // reservation): they live in SGPRs instead of spilled 64-bit VGPR pairs
+    const int Cm = ufl((int)H.C);
+    const int cap = ufl(c.cq_cap);
+    const int64_t obase = (int64_t)(((uint64_t)(uint32_t)ufl((int)(H.base >> 32)) << 32) |
+                                    (uint32_t)ufl((int)H.base));
     // members of chunk slot sl: BFS tree walk, or the re-walk buffer
-    auto clique_members = [&](int64_t sl, int (&mem)[K]) {
+    auto clique_members = [&](int sl, int (&mem)[K]) {
       if (bfs_ok) {
         BfsLevel<K, K>::prefix(q, bo.lvl, (uint32_t)sl, mem);
       } else {
@@ -1263,8 +1272,8 @@ void k_fused(FusedArgs A) {
       }
     };
     int ci = 0;
-    for (int64_t c0 = 0; c0 < Cm; c0 += c.cq_cap, ++ci) {
-      const int64_t c1 = min(Cm, c0 + (int64_t)c.cq_cap);
+    for (int c0 = 0; c0 < Cm; c0 += cap, ++ci) {
+      const int c1 = min(Cm, c0 + cap);
       if (tid == 0) H.tief[(ci + 1) & 1] = 0;   // last read before the previous chunk's end
       if (!bfs_ok) {
         c.c0 = c0;
@@ -1280,11 +1289,10 @@ void k_fused(FusedArgs A) {
         __syncthreads();
       }
       bool any = false;
-      for (int64_t sl = tid; sl < c1 - c0; sl += FWG) {
+      for (int sl = tid; sl < c1 - c0; sl += FWG) {
         int mem[K];
         clique_members(sl, mem);
-        const int64_t j = c0 + sl;
-        if (fused_epilogue_main<K, W>(c, H.base + j, mem)) {
+        if (fused_epilogue_main<K, W>(c, obase + (c0 + sl), mem)) {
           c.cq_ord[sl] |= 0x8000;
           any = true;
         }
@@ -1292,13 +1300,12 @@ void k_fused(FusedArgs A) {
       if (any) H.tief[ci & 1] = 1;
       __syncthreads();
       if (H.tief[ci & 1]) {
-        for (int64_t sl = tid; sl < c1 - c0; sl += FWG) {
+        for (int sl = tid; sl < c1 - c0; sl += FWG) {
           const uint32_t o = c.cq_ord[sl];
           if (!(o & 0x8000)) continue;
           int mem[K];
           clique_members(sl, mem);
-          const int64_t j = c0 + sl;
-          fused_epilogue_order<K, W>(c, H.base + j, mem);
+          fused_epilogue_order<K, W>(c, obase + (c0 + sl), mem);
         }
       }
       __syncthreads();
