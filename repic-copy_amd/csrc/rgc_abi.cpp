@@ -151,7 +151,8 @@ struct rgc_ctx {
   std::vector<float> times;
   std::vector<const char*> time_names;
   int64_t cap_cliques = 0;   // capacity of the per-clique output arrays
-  void* cursor_zeroed = nullptr;   // fused cursor already cleared on the stream for next run
+  void* cursor_zeroed = nullptr;
+  hipEvent_t ev_tail = nullptr;    // timing: recorded after each fused pass's stats copy   // fused cursor already cleared on the stream for next run
   std::vector<uint64_t> stamps;   // diagnostic build only
 };
 
@@ -590,6 +591,10 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
         TRY(mark(c, "d2h_stats"));
         HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOUT), D<void>(c, D_MGOUT), cur_off + 16,
                               hipMemcpyDeviceToHost, s));
+        if (c->timing) {
+          if (!c->ev_tail) HIPCHK(hipEventCreate(&c->ev_tail));
+          HIPCHK(hipEventRecord(c->ev_tail, s));
+        }
         HIPCHK(hipGetLastError());
         HIPCHK(hipStreamSynchronize(s));
         const int32_t* fst = ho.status;
@@ -717,10 +722,16 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
     out->members = want_members ? D<int32_t>(c, D_MEMBERS) : nullptr;
     out->order = multi ? D<uint8_t>(c, D_ORDER) : nullptr;
   }
-  TRY(mark(c, "end"));
+  // nothing enqueued since the fused passes' last sync -> no second round trip; their tail
+  // event closes the timeline
+  const bool fused_ran = all0 || !todo0.empty();
+  const bool tail_work = !fused_ran || !deferred.empty() || (flags & RGC_F_HOST_OUTPUTS);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(s));
-  if (all0 || !todo0.empty()) {
+  if (tail_work) {
+    TRY(mark(c, "end"));
+    HIPCHK(hipStreamSynchronize(s));
+  }
+  if (fused_ran) {
     // clear the cursor for the next run now, while the host is busy elsewhere
     HIPCHK(hipMemsetAsync(d_cur, 0, 16, s));
     c->cursor_zeroed = d_cur;
@@ -730,9 +741,10 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   if (c->timing) {
     c->times.clear();
     c->time_names.clear();
-    for (int i = 0; i + 1 < c->n_ev; ++i) {
+    for (int i = 0; i + 1 < c->n_ev || (!tail_work && i < c->n_ev); ++i) {
       float ms = 0.f;
-      HIPCHK(hipEventElapsedTime(&ms, c->events[i], c->events[i + 1]));
+      hipEvent_t e1 = i + 1 < c->n_ev ? c->events[i + 1] : c->ev_tail;
+      HIPCHK(hipEventElapsedTime(&ms, c->events[i], e1));
       c->times.push_back(ms);
       c->time_names.push_back(c->ev_names[i]);
     }
@@ -779,6 +791,7 @@ void rgc_ctx_destroy(rgc_ctx* c) {
   for (auto& b : c->h)
     if (b.p) (void)hipHostFree(b.p);
   for (auto e : c->events) (void)hipEventDestroy(e);
+  if (c->ev_tail) (void)hipEventDestroy(c->ev_tail);
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }

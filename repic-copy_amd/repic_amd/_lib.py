@@ -37,7 +37,7 @@ _u8p = C.POINTER(C.c_uint8)
 
 class BatchIn(C.Structure):
     _fields_ = [("n_mg", C.c_int32), ("k", C.c_int32), ("box_size", C.c_int64),
-                ("flags", C.c_uint32), ("box_off", _i64p), ("id_base", _i64p),
+                ("flags", C.c_uint32), ("box_off", C.c_void_p), ("id_base", C.c_void_p),
                 ("x", C.c_void_p), ("y", C.c_void_p), ("score", C.c_void_p),
                 ("dev_box_off", C.c_void_p), ("dev_id_base", C.c_void_p)]
 
@@ -187,24 +187,29 @@ class Context:
         pointer of id_base) sets ``F_DEVICE_META``: the offsets are not uploaded per run.
         Returns a :class:`Result` (views into context-owned memory that stay valid until the
         next ``run``)."""
-        box_off = np.ascontiguousarray(box_off, dtype=np.int64)
-        id_base = np.ascontiguousarray(id_base, dtype=np.int64)
+        # (kept lean: this runs once per batch inside the bench's timed region)
+        if not (type(box_off) is np.ndarray and box_off.dtype == np.int64
+                and box_off.flags.c_contiguous):
+            box_off = np.ascontiguousarray(box_off, dtype=np.int64)
+        if not (type(id_base) is np.ndarray and id_base.dtype == np.int64
+                and id_base.flags.c_contiguous):
+            id_base = np.ascontiguousarray(id_base, dtype=np.int64)
         assert box_off.shape == (n_mg * k + 1,) and id_base.shape == (n_mg,)
         keep = [box_off, id_base]
         if flags & F_DEVICE_INPUTS:
-            px, py, ps = (C.c_void_p(int(v)) for v in (x, y, score))
+            px, py, ps = int(x), int(y), int(score)
         else:
             x, y, score = (np.ascontiguousarray(v, dtype=np.float64) for v in (x, y, score))
             n = int(box_off[-1]) if len(box_off) else 0
             assert x.shape == y.shape == score.shape == (n,)
             keep += [x, y, score]
-            px, py, ps = (C.c_void_p(v.ctypes.data) for v in (x, y, score))
+            px, py, ps = x.ctypes.data, y.ctypes.data, score.ctypes.data
         dbo = did = None
         if dev_meta is not None:
             flags |= F_DEVICE_META
-            dbo, did = (C.c_void_p(int(v)) for v in dev_meta)
-        bi = BatchIn(n_mg, k, int(box_size), flags, box_off.ctypes.data_as(_i64p),
-                     id_base.ctypes.data_as(_i64p), px, py, ps, dbo, did)
+            dbo, did = int(dev_meta[0]), int(dev_meta[1])
+        bi = BatchIn(n_mg, k, int(box_size), flags, box_off.ctypes.data, id_base.ctypes.data,
+                     px, py, ps, dbo, did)
         bo = BatchOut()
         _check(lib.rgc_run(self._p, C.byref(bi), C.byref(bo)))
         del keep

@@ -39,8 +39,7 @@ class Runner:
 
     def run(self):
         bi = _lib.BatchIn(batch.n_mg, cfg.k, cfg.box, _lib.F_TIMING,
-                          batch.box_off.ctypes.data_as(C.POINTER(C.c_int64)),
-                          batch.id_base.ctypes.data_as(C.POINTER(C.c_int64)),
+                          batch.box_off.ctypes.data, batch.id_base.ctypes.data,
                           C.c_void_p(batch.x.ctypes.data), C.c_void_p(batch.y.ctypes.data),
                           C.c_void_p(batch.score.ctypes.data))
         bo = _lib.BatchOut()
