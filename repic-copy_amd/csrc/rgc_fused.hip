@@ -1010,7 +1010,12 @@ void k_fused(FusedArgs A) {
   // each box's edge bitmask for the fill.
   uint32_t* ccsz = reinterpret_cast<uint32_t*>(S.vrank);   // packed u16 CC sizes (P2-P3)
   for (int q = tid; q < (n + 1) / 2; q += FWG) ccsz[q] = 0;
-  for (int ts = tid; ts < n; ts += FWG) {
+  // boustrophedon box order: odd rounds walk their FWG positions backwards, so a thread that
+  // took a low-picker box (most grids to search) in one round takes a high-picker box (fewest)
+  // in the next; K = 3, ~900 boxes: at most 6 instead of 9 column ranges per thread
+  for (int r0 = 0, odd = 0; r0 < n; r0 += FWG, odd ^= 1) {
+    const int ts = odd ? r0 + FWG - 1 - tid : r0 + tid;
+    if (ts >= n) continue;
     Stencil st;
     stencil_setup<K, W>(st, ts, S, G);
     uint32_t mask;
@@ -1035,7 +1040,9 @@ void k_fused(FusedArgs A) {
     // union-find, balanced across lanes whatever the degrees).  Without room: union per box.
     const bool src_ok = 2 * E <= A.ecap;
     uint16_t* esrc = S.dst + E;
-    for (int ts = tid; ts < n; ts += FWG) {
+    for (int r0 = 0, odd = 0; r0 < n; r0 += FWG, odd ^= 1) {   // same order as the count
+      const int ts = odd ? r0 + FWG - 1 - tid : r0 + tid;
+      if (ts >= n) continue;
       const int i = ts;
       const int base = S.fwd[i], cnt = (int)S.fwd[i + 1] - base;
       if (cnt == 0) continue;
