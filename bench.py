@@ -107,8 +107,8 @@ def cpu_baseline(cfg, mgs, budget_s=12.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--n_mg", type=int, default=None, help="micrographs per GPU")
     ap.add_argument("--seed", type=int, default=0)

@@ -713,13 +713,28 @@ __device__ __forceinline__ int pairs_count(const Stencil& st, const FShared& S, 
                                            uint32_t* mask_out) {
   uint32_t mask = 0;
   int cnt = 0, kk = 0;
+  // f32 layout: reject in f32 first.  An edge needs both overlaps > (6/13) B, i.e. |dx| and
+  // |dy| < (7/13) B = 0.5385 B; the f32 difference of two exact f32 values is within 2^-24 of
+  // the true one, so |dx| >= 0.54 B (as computed) can never be an edge.
+  const float rej = 0.54f * (float)B;
+  const float ax = (float)st.a.x, ay = (float)st.a.y;
   for (int q = st.p + 1; q < K; ++q) {
 #pragma unroll
     for (int d = -1; d <= 1; ++d) {
       int lo, hi;
       stencil_range(st, S, H, q, d, lo, hi);
       for (int t = lo; t < hi; ++t, ++kk) {
-        if (edge_test(st.a, ld_xy<W>(S, t), B, two_b2, i_lo, i_hi)) {
+        bool e;
+        if constexpr (W) {
+          e = edge_test(st.a, ld_xy<W>(S, t), B, two_b2, i_lo, i_hi);
+        } else {
+          const float2 bf = reinterpret_cast<const float2*>(S.sxy)[t];
+          e = false;
+          if (fabsf(ax - bf.x) < rej && fabsf(ay - bf.y) < rej)
+            e = edge_test(st.a, make_double2((double)bf.x, (double)bf.y), B, two_b2, i_lo,
+                          i_hi);
+        }
+        if (e) {
           ++cnt;
           mask |= (kk < 32) ? (1u << kk) : 0u;
         }
