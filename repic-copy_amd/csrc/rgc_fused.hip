@@ -1248,22 +1248,11 @@ void k_fused(FusedArgs A) {
       const int b = xbucket(v.x);
       const int lo = bcnt[b], hi = bcnt[b + 1];
       uint32_t rk = lo;
-      if constexpr (W) {
-        for (int u = lo; u < hi; ++u) {
-          const int tu = blist[u];
-          const double2 w = ld_xy<W>(S, tu);
-          const int ui = S.citems[tu];
-          rk += (w.x < v.x) || (w.x == v.x && (w.y < v.y || (w.y == v.y && ui < vi)));
-        }
-      } else {
-        // f32 layout: the f64 values are the exact f32 ones, so f32 compares order them alike
-        const float2 vf = reinterpret_cast<const float2*>(S.sxy)[t];
-        for (int u = lo; u < hi; ++u) {
-          const int tu = blist[u];
-          const float2 w = reinterpret_cast<const float2*>(S.sxy)[tu];
-          const int ui = S.citems[tu];
-          rk += (w.x < vf.x) || (w.x == vf.x && (w.y < vf.y || (w.y == vf.y && ui < vi)));
-        }
+      for (int u = lo; u < hi; ++u) {
+        const int tu = blist[u];
+        const double2 w = ld_xy<W>(S, tu);
+        const int ui = S.citems[tu];
+        rk += (w.x < v.x) || (w.x == v.x && (w.y < v.y || (w.y == v.y && ui < vi)));
       }
       S.vrank[t] = (uint16_t)rk;
     }
