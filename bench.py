@@ -104,6 +104,48 @@ def cpu_baseline(cfg, mgs, budget_s=12.0):
                       f"(reference get_jaccard structure), 1 process, {dt:.1f} s"}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(n):
+    """``--gpus N`` without a torch.distributed launcher: start N fresh child processes of this
+    script, one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), and
+    exit with the worst child status.  Runs before anything touches the GPU (the parent never
+    initialises HIP); rank 0's JSON line reaches the inherited stdout."""
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, WORLD_SIZE=str(n), RANK=str(r), LOCAL_RANK=str(r),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    # a failed rank would leave the others blocked in a collective: stop them (our own
+    # children, by handle)
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc not in (None, 0)]
+        if bad:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            return bad[0]
+        if all(rc == 0 for rc in rcs):
+            return 0
+        time.sleep(0.05)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -118,10 +160,20 @@ def main():
                     help="PCIe-inclusive variant (never the headline value): host x/y/score and "
                          "offsets are uploaded and every per-clique output is copied back to "
                          "pinned host memory inside each step")
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
-    import torch
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.launch_check:   # test hook: the launcher's rank layout, no GPU work
+        print(json.dumps({k_: os.environ.get(k_) for k_ in
+                          ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR")}), flush=True)
+        return
+
+    import torch
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # RGC_BENCH_DEVICE / RGC_DIST_BACKEND: test hooks (two ranks on one GPU over gloo);

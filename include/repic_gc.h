@@ -40,6 +40,8 @@ extern "C" {
 #define RGC_F_DEVICE_META  128u  /* dev_box_off / dev_id_base hold HBM-resident copies of
                                     box_off (as int32) and id_base: no offset upload per run
                                     (the host arrays are still read for launch planning) */
+#define RGC_F_EDGES        256u  /* test hook: also record every JI > 0.3 edge with its f64 JI
+                                    (rgc_last_edges); outputs are unchanged */
 
 /* per-micrograph status (rgc_batch_out.status) */
 #define RGC_OK          0   /* outputs written as in get_cliques.py:215-229 */
@@ -114,6 +116,11 @@ void rgc_ctx_destroy(rgc_ctx* ctx);
 int rgc_run(rgc_ctx* ctx, const rgc_batch_in* in, rgc_batch_out* out);
 /* Per-kernel device milliseconds of the last rgc_run with RGC_F_TIMING; returns the count. */
 int rgc_kernel_times(rgc_ctx* ctx, int max_n, float* ms, const char** names);
+
+/* Test hook (RGC_F_EDGES): the JI > 0.3 edges of the last rgc_run as host arrays (batch box
+ * indices u < v by picker, JI in the reference's f64 op order, get_cliques.py:40-46,59-69),
+ * valid until the next rgc_run; returns the edge count (order unspecified). */
+int64_t rgc_last_edges(rgc_ctx* ctx, const int32_t** u, const int32_t** v, const double** ji);
 
 int rgc_parse_files(const char* const* paths, int64_t n_files, int n_threads, rgc_parsed** out);
 void rgc_parsed_free(rgc_parsed* p);

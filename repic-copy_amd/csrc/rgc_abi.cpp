@@ -59,11 +59,13 @@ enum DevBufId {
   D_BOXOFF, D_CELLOFF, D_IDBASE, D_GRID, D_CELLSTART, D_SX, D_SY, D_SBOX, D_SPICK, D_SMG, D_BMG,
   D_BPICK, D_FWDCNT, D_FWDOFF, D_TILES, D_TOTAL, D_EDST, D_EJI, D_PARENT, D_HASEDGE, D_CSIZE,
   D_STAT, D_INSKEY, D_COMPMIN, D_CCOUNT, D_COFF, D_INCL, D_VLIST, D_VSORT, D_VROW, D_MGOFF,
+  // RGC_F_EDGES test hook
+  D_EU, D_EV, D_EJIOUT,
   D_COUNT
 };
 enum HostBufId {
   H_FSTAGE, H_STAGE, H_TOTAL, H_MGOUT, H_STAT, H_MGOFF, H_ROWS, H_W, H_CONF, H_CONS, H_MEMBERS,
-  H_ORDER, H_COUNT
+  H_ORDER, H_EU, H_EV, H_EJIOUT, H_COUNT
 };
 
 struct Buf {
@@ -77,6 +79,9 @@ struct Buf {
 constexpr int LDS_BLOCK = 1280;
 constexpr int LDS_BLOCKS = 128;
 constexpr int FUSED_WG = 512;
+// device cursors after the per-micrograph block: [0] clique reservation, [1] edges of finished
+// micrographs, [2] edge-dump reservation (RGC_F_EDGES), [3] spare
+constexpr size_t CUR_BYTES = 32;
 static int lds_blocks(int bytes) { return (bytes + LDS_BLOCK - 1) / LDS_BLOCK; }
 
 // One fused launch configuration: micrographs of <= nmax boxes, forward-edge capacity ecap,
@@ -151,6 +156,8 @@ struct rgc_ctx {
   std::vector<float> times;
   std::vector<const char*> time_names;
   int64_t cap_cliques = 0;   // capacity of the per-clique output arrays
+  int64_t cap_edges = 0;     // RGC_F_EDGES: capacity of the edge dump
+  int64_t n_edge_dump = 0;   // RGC_F_EDGES: edges of the last run (host copies in H_EU..)
   void* cursor_zeroed = nullptr;
   hipEvent_t ev_tail = nullptr;    // timing: recorded after each fused pass's stats copy   // fused cursor already cleared on the stream for next run
   std::vector<uint64_t> stamps;   // diagnostic build only
@@ -215,6 +222,14 @@ static int ensure_outputs(rgc_ctx* c, int64_t need, int64_t keep, int k, bool me
   TRY(ensure_dev(c, D_CONS, need * 4, keep * 4));
   if (members) TRY(ensure_dev(c, D_MEMBERS, need * k * 4, keep * k * 4));
   if (multi) TRY(ensure_dev(c, D_ORDER, need * k, keep * k));
+  return 0;
+}
+
+// Grow the RGC_F_EDGES dump arrays to `need` edges, keeping the first `keep`.
+static int ensure_edges(rgc_ctx* c, int64_t need, int64_t keep) {
+  TRY(ensure_dev(c, D_EU, need * 4, keep * 4));
+  TRY(ensure_dev(c, D_EV, need * 4, keep * 4));
+  TRY(ensure_dev(c, D_EJIOUT, need * 8, keep * 8));
   return 0;
 }
 
@@ -394,6 +409,8 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   const int get_cc = (flags & RGC_F_GET_CC) ? 1 : 0;
   const int multi = (flags & RGC_F_MULTI_OUT) ? 1 : 0;
   const bool want_members = (flags & (RGC_F_MEMBERS | RGC_F_MULTI_OUT)) != 0;
+  const bool want_edges = (flags & RGC_F_EDGES) != 0;
+  c->n_edge_dump = 0;
   const double B = (double)in->box_size;
   const double two_b2 = (double)(2 * in->box_size * in->box_size);
   c->timing = (flags & RGC_F_TIMING) != 0;
@@ -403,8 +420,8 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   // the fused kernels' reservation cursor (16 B) sits right after the per-micrograph block,
   // so one copy returns both
   const size_t cur_off = (mgout_bytes(n_mg) + 15) & ~(size_t)15;
-  TRY(ensure_host(c, H_MGOUT, cur_off + 16));
-  TRY(ensure_dev(c, D_MGOUT, cur_off + 16));
+  TRY(ensure_host(c, H_MGOUT, cur_off + CUR_BYTES));
+  TRY(ensure_dev(c, D_MGOUT, cur_off + CUR_BYTES));
   const MgOut ho = mgout_bind(H<void>(c, H_MGOUT), n_mg);
   const MgOut dout = mgout_bind(D<void>(c, D_MGOUT), n_mg);
   std::memset(out, 0, sizeof(*out));
@@ -474,6 +491,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   // f64 coordinates; pass 2: the edge-capacity overflows of pass 1 with the whole LDS.  What
   // is still deferred (or too large for LDS) runs through the multi-kernel path.
   int64_t fused_total = 0;
+  int64_t fused_edges = 0;   // RGC_F_EDGES: edges dumped by the fused passes
   int64_t E_total = 0;
   std::vector<int32_t> deferred;
   std::vector<int32_t> todo0;
@@ -511,11 +529,14 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   }
   if (all0 || !todo0.empty()) {
     if (c->cap_cliques < 4096) c->cap_cliques = std::max<int64_t>(4096, N);
+    if (want_edges && c->cap_edges < 4 * N + 4096) c->cap_edges = 4 * N + 4096;
     for (int attempt = 0; attempt < 2; ++attempt) {
       TRY(ensure_outputs(c, c->cap_cliques, 0, k, want_members, multi != 0));
+      if (want_edges) TRY(ensure_edges(c, c->cap_edges, 0));
       // the previous run cleared the cursor after its last read (off this run's critical
       // path); otherwise (first run, moved buffer, regrow attempt) clear it here
-      if (attempt > 0 || c->cursor_zeroed != d_cur) HIPCHK(hipMemsetAsync(d_cur, 0, 16, s));
+      if (attempt > 0 || c->cursor_zeroed != d_cur)
+        HIPCHK(hipMemsetAsync(d_cur, 0, CUR_BYTES, s));
       c->cursor_zeroed = nullptr;
       FusedArgs A;
       A.k = k; A.flags = get_cc | (multi << 1) | (want_members ? 32 : 0);
@@ -528,6 +549,10 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
       A.members = want_members ? D<int32_t>(c, D_MEMBERS) : nullptr;
       A.order = multi ? D<uint8_t>(c, D_ORDER) : nullptr;
       A.stamps = nullptr;
+      A.eu = want_edges ? D<int32_t>(c, D_EU) : nullptr;
+      A.ev = want_edges ? D<int32_t>(c, D_EV) : nullptr;
+      A.eji = want_edges ? D<double>(c, D_EJIOUT) : nullptr;
+      A.ecap_out = c->cap_edges;
 #ifdef RGC_STAMPS
       TRY(ensure_dev(c, D_STAMPS, 3 * (size_t)n_mg * 16 * 8));
       HIPCHK(hipMemsetAsync(D<void>(c, D_STAMPS), 0, 3 * (size_t)n_mg * 128, s));
@@ -589,7 +614,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
                         (le > 0 ? hipGetErrorString((hipError_t)le) : "unsupported k"));
         }
         TRY(mark(c, "d2h_stats"));
-        HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOUT), D<void>(c, D_MGOUT), cur_off + 16,
+        HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOUT), D<void>(c, D_MGOUT), cur_off + CUR_BYTES,
                               hipMemcpyDeviceToHost, s));
         if (c->timing) {
           if (!c->ev_tail) HIPCHK(hipEventCreate(&c->ev_tail));
@@ -619,12 +644,16 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
       c->stamps.resize(n0w * 16);
       HIPCHK(hipMemcpy(c->stamps.data(), D<void>(c, D_STAMPS), n0w * 128, hipMemcpyDeviceToHost));
 #endif
-      if (!overflow && fused_total <= c->cap_cliques) {
+      fused_edges = (int64_t)h_cur[2];
+      const bool edge_over = want_edges && fused_edges > c->cap_edges;
+      if (!overflow && fused_total <= c->cap_cliques && !edge_over) {
         for (int32_t m : todo) deferred.push_back(m);
         break;
       }
       if (attempt == 1) return fail("internal: output overflow after regrow");
-      c->cap_cliques = fused_total + fused_total / 8 + 1024;   // grow and re-run once
+      if (edge_over) c->cap_edges = fused_edges + fused_edges / 8 + 1024;
+      if (overflow || fused_total > c->cap_cliques)   // grow and re-run once
+        c->cap_cliques = fused_total + fused_total / 8 + 1024;
       c->n_ev = 0;
     }
     E_total = (int64_t)h_cur[1];   // finished micrographs
@@ -668,6 +697,13 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
     TRY(mark(c, "k_remap"));
     launch_remap(s, Cm, k, D<int32_t>(c, D_ORIG), D<int32_t>(c, D_CONS) + fused_total,
                  D<int32_t>(c, D_MEMBERS) + fused_total * k);
+    if (want_edges) {
+      TRY(ensure_edges(c, fused_edges + Em, fused_edges));
+      launch_dump_edges(s, (int)acc, D<int64_t>(c, D_FWDOFF), D<int32_t>(c, D_EDST),
+                        D<double>(c, D_EJI), D<int32_t>(c, D_ORIG), D<int32_t>(c, D_EU) + fused_edges,
+                        D<int32_t>(c, D_EV) + fused_edges, D<double>(c, D_EJIOUT) + fused_edges);
+      fused_edges += Em;
+    }
     for (int i = 0; i < ns; ++i) {
       const int m = deferred[i];
       const MgStat& t = sst[i];
@@ -688,6 +724,20 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   out->n_cliques = C_total;
   out->n_edges = E_total;
 
+  if (want_edges) {
+    const int64_t ne = fused_edges;
+    TRY(ensure_host(c, H_EU, ne * 4));
+    TRY(ensure_host(c, H_EV, ne * 4));
+    TRY(ensure_host(c, H_EJIOUT, ne * 8));
+    if (ne) {
+      HIPCHK(hipMemcpyAsync(H<void>(c, H_EU), D<void>(c, D_EU), ne * 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(H<void>(c, H_EV), D<void>(c, D_EV), ne * 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(H<void>(c, H_EJIOUT), D<void>(c, D_EJIOUT), ne * 8,
+                            hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    c->n_edge_dump = ne;
+  }
   if (flags & RGC_F_HOST_OUTPUTS) {
     TRY(mark(c, "d2h"));
     const int64_t C = C_total;
@@ -733,7 +783,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   }
   if (fused_ran) {
     // clear the cursor for the next run now, while the host is busy elsewhere
-    HIPCHK(hipMemsetAsync(d_cur, 0, 16, s));
+    HIPCHK(hipMemsetAsync(d_cur, 0, CUR_BYTES, s));
     c->cursor_zeroed = d_cur;
   }
 
@@ -810,6 +860,14 @@ int rgc_kernel_times(rgc_ctx* c, int max_n, float* ms, const char** names) {
     if (names) names[i] = c->time_names[i];
   }
   return (int)c->times.size();
+}
+
+int64_t rgc_last_edges(rgc_ctx* c, const int32_t** u, const int32_t** v, const double** ji) {
+  if (!c) return fail("null ctx");
+  if (u) *u = H<int32_t>(c, H_EU);
+  if (v) *v = H<int32_t>(c, H_EV);
+  if (ji) *ji = H<double>(c, H_EJIOUT);
+  return c->n_edge_dump;
 }
 
 uint64_t rgc_py_hash_node(double x, double y, int64_t id) { return pyset::hash_node(x, y, id); }

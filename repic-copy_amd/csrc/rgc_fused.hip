@@ -1084,6 +1084,26 @@ void k_fused(FusedArgs A) {
       }
       __syncthreads();
     }
+    if (A.eu) {
+      // RGC_F_EDGES test hook: the edge list with the reference's f64 JI (get_cliques.py:40-46)
+      if (tid == 0) H.base = (int64_t)atomicAdd(A.cursor + 2, (unsigned long long)E);
+      __syncthreads();
+      const int64_t eb = H.base;
+      if (eb + E <= A.ecap_out) {
+        for (int i = tid; i < n; i += FWG) {
+          const double2 a = ld_xy<W>(S, i);
+          for (int e = S.fwd[i]; e < (int)S.fwd[i + 1]; ++e) {
+            const int h = S.dst[e];
+            const double2 b = ld_xy<W>(S, h);
+            A.eu[eb + e] = b0 + S.citems[i];
+            A.ev[eb + e] = b0 + S.citems[h];
+            A.eji[eb + e] = jaccard(a.x, a.y, b.x, b.y, B, two_b2);
+          }
+        }
+      }
+      __syncthreads();
+      if (tid == 0) H.base = 0;
+    }
     STAMP(5);   // fill + sort
   }
   if (H.status != 0) {

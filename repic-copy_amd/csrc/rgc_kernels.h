@@ -84,6 +84,12 @@ struct FusedArgs {
   int32_t* members;
   uint8_t* order;
   unsigned long long* stamps;   // diagnostic build (RGC_STAMPS) only: 8 stamps per WG
+  // RGC_F_EDGES test hook (nullptr otherwise): every JI > 0.3 edge as (u, v, JI) with batch
+  // box indices, reserved per micrograph on cursor[2]; nothing is written past ecap_out
+  int32_t* eu;
+  int32_t* ev;
+  double* eji;
+  int64_t ecap_out;
 };
 
 int fused_lds_bytes(int nmax, int ecap, bool wide);
@@ -95,6 +101,9 @@ void launch_gather(hipStream_t stream, int n_sub, int k, const int32_t* sub_mg,
                    int32_t* orig);
 void launch_remap(hipStream_t stream, int64_t C, int k, const int32_t* orig, int32_t* consensus,
                   int32_t* members);
+void launch_dump_edges(hipStream_t stream, int N, const int64_t* fwd_off, const int32_t* e_dst,
+                       const double* e_ji, const int32_t* orig, int32_t* eu, int32_t* ev,
+                       double* eji);
 
 struct CliqueArgsHost {
   int k;

@@ -698,7 +698,31 @@ __global__ __launch_bounds__(WG) void k_remap(int64_t C, int k, const int32_t* _
   for (int i = 0; i < k; ++i) members[j * k + i] = orig[members[j * k + i]];
 }
 
+// RGC_F_EDGES test hook: the sub-batch's edge list (u, v, JI) in batch box indices.
+__global__ __launch_bounds__(WG) void k_dump_edges(int N, const int64_t* __restrict__ fwd_off,
+                                                   const int32_t* __restrict__ e_dst,
+                                                   const double* __restrict__ e_ji,
+                                                   const int32_t* __restrict__ orig, int32_t* eu,
+                                                   int32_t* ev, double* eji) {
+  const int g = blockIdx.x * WG + threadIdx.x;
+  if (g >= N) return;
+  for (int64_t e = fwd_off[g]; e < fwd_off[g + 1]; ++e) {
+    eu[e] = orig[g];
+    ev[e] = orig[e_dst[e]];
+    eji[e] = e_ji[e];
+  }
+}
+
 // ----------------------------------------------------------------------------- launchers
+void launch_dump_edges(hipStream_t stream, int N, const int64_t* fwd_off, const int32_t* e_dst,
+                       const double* e_ji, const int32_t* orig, int32_t* eu, int32_t* ev,
+                       double* eji) {
+  const int nb = (N + WG - 1) / WG;
+  if (nb > 0)
+    hipLaunchKernelGGL(k_dump_edges, dim3(nb), dim3(WG), 0, stream, N, fwd_off, e_dst, e_ji, orig,
+                       eu, ev, eji);
+}
+
 void launch_gather(hipStream_t stream, int n_sub, int k, const int32_t* sub_mg,
                    const int32_t* box_off, const int32_t* sub_box_off, const double* x,
                    const double* y, const double* s, double* ox, double* oy, double* os,

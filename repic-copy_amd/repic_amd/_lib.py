@@ -23,7 +23,7 @@ if not os.path.exists(LIB_PATH):
 lib = C.CDLL(LIB_PATH)
 
 F_GET_CC, F_MULTI_OUT, F_DEVICE_INPUTS, F_HOST_OUTPUTS, F_TIMING = 1, 2, 4, 8, 16
-F_MEMBERS, F_NO_FUSED, F_DEVICE_META = 32, 64, 128
+F_MEMBERS, F_NO_FUSED, F_DEVICE_META, F_EDGES = 32, 64, 128, 256
 OK, NO_EDGES, NO_CLIQUES = 0, 1, 2
 PARSE_OK, PARSE_INDEX, PARSE_VALUE, PARSE_ASSERT, PARSE_FALLBACK, PARSE_OSERROR = range(6)
 MAX_K = 8
@@ -63,6 +63,9 @@ lib.rgc_ctx_create.argtypes = [C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]
 lib.rgc_ctx_destroy.argtypes = [C.c_void_p]
 lib.rgc_ctx_destroy.restype = None
 lib.rgc_run.argtypes = [C.c_void_p, C.POINTER(BatchIn), C.POINTER(BatchOut)]
+lib.rgc_last_edges.argtypes = [C.c_void_p, C.POINTER(_i32p), C.POINTER(_i32p),
+                               C.POINTER(_f64p)]
+lib.rgc_last_edges.restype = C.c_int64
 lib.rgc_kernel_times.argtypes = [C.c_void_p, C.c_int, _f32p, C.POINTER(C.c_char_p)]
 lib.rgc_parse_files.argtypes = [C.POINTER(C.c_char_p), C.c_int64, C.c_int,
                                 C.POINTER(C.POINTER(Parsed))]
@@ -76,7 +79,7 @@ lib.rgc_test_epilogue.argtypes = [C.c_int, _f64p, _f64p, _f64p, C.POINTER(C.c_in
                                   C.POINTER(C.c_int8), _f32p, _f32p]
 
 EXPORTS = ["rgc_abi_version", "rgc_last_error", "rgc_device_count", "rgc_ctx_create",
-           "rgc_ctx_destroy", "rgc_run", "rgc_kernel_times", "rgc_parse_files",
+           "rgc_ctx_destroy", "rgc_run", "rgc_kernel_times", "rgc_last_edges", "rgc_parse_files",
            "rgc_parsed_free", "rgc_py_hash_node", "rgc_py_set_order", "rgc_test_epilogue"]
 
 
@@ -214,6 +217,17 @@ class Context:
         _check(lib.rgc_run(self._p, C.byref(bi), C.byref(bo)))
         del keep
         return Result(bo, n_mg, k, flags)
+
+    def last_edges(self):
+        """Test hook: (u, v, ji) copies of the JI > 0.3 edges of the last run with F_EDGES
+        (batch box indices; order unspecified)."""
+        u, v, j = _i32p(), _i32p(), _f64p()
+        n = _check(lib.rgc_last_edges(self._p, C.byref(u), C.byref(v), C.byref(j)))
+        if n == 0:
+            return np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0)
+        return (np.ctypeslib.as_array(u, shape=(n,)).copy(),
+                np.ctypeslib.as_array(v, shape=(n,)).copy(),
+                np.ctypeslib.as_array(j, shape=(n,)).copy())
 
     def kernel_times(self):
         n = lib.rgc_kernel_times(self._p, 0, None, None)

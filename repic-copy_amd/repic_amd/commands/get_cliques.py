@@ -12,6 +12,7 @@ Extra options (do not change outputs): ``--batch_boxes`` (boxes per device batch
 """
 from __future__ import annotations
 
+import argparse
 import os
 import shutil
 import sys
@@ -21,7 +22,7 @@ from pathlib import Path
 import numpy as np
 
 from .. import _lib
-from ..dist import exclusive_offsets, shard_bounds
+from ..dist import agree, pair_work, reduce_counts, shard_bounds
 from ..ingest import DirIndex, list_methods, micrograph_names, plan, probe_start_method
 from ..pipeline import Batch, run_batch, split_batches
 from ..writers import Writer, consensus_coords, constraint_matrix, multi_out_coords
@@ -47,6 +48,15 @@ def add_arguments(parser):
                         help="host BOX-parser threads (does not change outputs)")
     parser.add_argument("--device", type=int, default=None,
                         help="HIP device (default: $LOCAL_RANK or 0)")
+    # tests only: JSON {picker: [names in readdir order]} replayed instead of os.listdir, so
+    # global box ids (and the consensus tie-breaks) match a recorded reference run
+    parser.add_argument("--listing", type=_load_listing, default=None, help=argparse.SUPPRESS)
+
+
+def _load_listing(path):
+    import json
+    with open(path) as f:
+        return json.load(f)
 
 
 def _del_dir(path):
@@ -75,13 +85,43 @@ def main(args):
         ctx.close()
 
 
+def _methods_after_reset(in_dir, out_dir):
+    """The picker list the reference will see once out_dir is deleted (get_cliques.py:77-82):
+    out_dir itself is not a picker even when it lies inside in_dir."""
+    out = os.path.realpath(out_dir)
+    return [m for m in list_methods(in_dir)
+            if os.path.realpath(os.path.join(in_dir, m)) != out]
+
+
+def _shard_weights(in_dir, methods, index, names):
+    """Per-micrograph pair-loop work estimate (sum over picker pairs of the product of the BOX
+    file sizes, a proxy for n_j * n_l) for balanced contiguous shards."""
+    w = np.empty(len(names))
+    for i, name in enumerate(names):
+        base = name.replace(".box", "")
+        sizes = []
+        for p, m in enumerate(methods):
+            fl = [name] if p == 0 else index.glob(m, f"*{base}*")
+            try:
+                sizes.append(sum(os.stat(os.path.join(in_dir, m, f)).st_size for f in fl))
+            except OSError:
+                sizes.append(0)
+        w[i] = 1.0 + pair_work(sizes)
+    return w
+
+
 def _main(args, ctx, world, rank):
     dist = None
     if world > 1:
         import torch.distributed as dist
         if not dist.is_initialized():
-            dist.init_process_group("gloo")   # control-plane only: 8-byte exchanges
+            dist.init_process_group("gloo")   # control-plane only: a few int64 per rank
     assert os.path.exists(args.in_dir), "Error - input directory does not exist"
+    # checked before anything is deleted: the device kernels are compiled for k <= MAX_K
+    k_pre = len(_methods_after_reset(args.in_dir, args.out_dir))
+    if k_pre > _lib.MAX_K:
+        raise _lib.RGCError(f"{k_pre} picker directories in {args.in_dir}: this build supports "
+                            f"at most {_lib.MAX_K} (no output was deleted or written)")
     if rank == 0:
         _del_dir(args.out_dir)
     if dist is not None:
@@ -96,43 +136,60 @@ def _main(args, ctx, world, rank):
     names = micrograph_names(index, methods)
     lo, hi = 0, len(names)
     if dist is not None:
-        b = shard_bounds(np.ones(len(names)), world)
+        b = shard_bounds(_shard_weights(args.in_dir, methods, index, names), world)
         lo, hi = b[rank], b[rank + 1]
+    k = len(methods)
     t_plan = time.time()
-    mgs, crash, consumed = plan(args.in_dir, methods, index, order=names[lo:hi],
-                                n_threads=getattr(args, "threads", None))
-    id_off = 0
+    mgs, results, err, consumed = [], {}, None, 0
+    try:
+        mgs, crash, consumed = plan(args.in_dir, methods, index, order=names[lo:hi],
+                                    n_threads=getattr(args, "threads", None))
+    except Exception as e:  # noqa: BLE001 - re-raised by agree() after the exchange
+        err = e
     if dist is not None:
-        id_off, _ = exclusive_offsets(consumed)
+        # global box-id offset of this shard (the one data exchange), with failure agreement
+        cons = agree(err, [consumed])
+        id_off = sum(c[0] for c in cons[:rank])
         for mg in mgs:
             mg.id_base += id_off
-    k = len(methods)
+    elif err is not None:
+        raise err
     ok = [mg for mg in mgs if mg.status == "ok"]
     t_plan = time.time() - t_plan
-    results = {}
     t_dev = 0.0
-    if ok:
-        counts = [sum(c.n for c in mg.coords) for mg in ok]
-        for m0, m1 in split_batches(counts, getattr(args, "batch_boxes", 1 << 25)):
-            part = ok[m0:m1]
-            batch = Batch.pack(k, args.box_size, [[(c.x, c.y, c.s) for c in mg.coords]
-                                                 for mg in part],
-                               id_bases=[mg.id_base for mg in part])
-            t0 = time.time()
-            res = run_batch(ctx, batch, get_cc=args.get_cc, multi_out=args.multi_out)
-            t_dev += time.time() - t0
-            for j, mg in enumerate(part):
-                results[id(mg)] = (batch, j, res[j])
+    n_edges = n_cliques = 0
+    try:
+        if ok:
+            counts = [sum(c.n for c in mg.coords) for mg in ok]
+            for m0, m1 in split_batches(counts, getattr(args, "batch_boxes", 1 << 25)):
+                part = ok[m0:m1]
+                batch = Batch.pack(k, args.box_size, [[(c.x, c.y, c.s) for c in mg.coords]
+                                                     for mg in part],
+                                   id_bases=[mg.id_base for mg in part])
+                t0 = time.time()
+                res = run_batch(ctx, batch, get_cc=args.get_cc, multi_out=args.multi_out)
+                t_dev += time.time() - t0
+                for j, mg in enumerate(part):
+                    results[id(mg)] = (batch, j, res[j])
+                    n_edges += res[j].n_edges
+                    n_cliques += len(res[j].w)
+    except Exception as e:  # noqa: BLE001
+        if dist is None:
+            raise
+        err = e
     # first micrograph (global index) at which the reference would raise
     fail = None
-    for i, mg in enumerate(mgs):
-        if mg.status == "crash" or (mg.status == "ok" and
-                                    results[id(mg)][2].status != _lib.OK):
-            fail = lo + i
-            break
+    if err is None:
+        for i, mg in enumerate(mgs):
+            if mg.status == "crash" or (mg.status == "ok" and
+                                        results[id(mg)][2].status != _lib.OK):
+                fail = lo + i
+                break
     if dist is not None:
-        from ..dist import first_failure
-        gfail = first_failure(fail)
+        big = np.iinfo(np.int64).max
+        rows = agree(err, [big if fail is None else fail])
+        gfail = min(r[0] for r in rows)
+        gfail = None if gfail == big else gfail
     else:
         gfail = fail
     share = (t_plan + t_dev) / max(1, len(mgs))
@@ -141,6 +198,12 @@ def _main(args, ctx, world, rank):
         _write_all(args, mgs, results, methods, k, lo, fail, gfail, share, writer)
     finally:
         writer.close()
+        if dist is not None:
+            # node-level counters: one reduction at the end of the run
+            tot = reduce_counts([len(ok), n_edges, n_cliques])
+            if rank == 0:
+                print(f"get_cliques: {tot[0]} micrographs, {tot[1]} edges, {tot[2]} cliques "
+                      f"on {world} ranks")
     sys.stdout.flush()
 
 

@@ -45,6 +45,41 @@ def exclusive_offsets(values, group=None, device=None):
     return sum(vals[:r]), sum(vals)
 
 
+def gather_rows(values, group=None, device=None):
+    """All-gather one int64 vector per rank -> list (by rank) of lists."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([int(v) for v in values], dtype=torch.int64, device=device)
+    world = dist.get_world_size(group)
+    allv = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(allv, t, group=group)
+    return [[int(v) for v in a.tolist()] for a in allv]
+
+
+class PeerFailure(RuntimeError):
+    """Another rank failed (its own exception is raised there)."""
+
+
+def agree(local_exc, values=(), group=None, device=None):
+    """One exchange after fallible per-rank work: every rank learns whether any rank failed
+    (so no rank is left blocked in a later collective) and gets the gathered ``values``.
+    Re-raises this rank's exception, or raises PeerFailure naming the failed ranks."""
+    rows = gather_rows([0 if local_exc is None else 1] + list(values), group, device)
+    bad = [r for r, row in enumerate(rows) if row[0]]
+    if local_exc is not None:
+        raise local_exc
+    if bad:
+        raise PeerFailure(f"get_cliques failed on rank(s) {bad}")
+    return [row[1:] for row in rows]
+
+
+def pair_work(sizes):
+    """Pair-loop work estimate of one micrograph from its k per-picker box counts (or file
+    sizes): sum over picker pairs j < l of n_j * n_l (get_cliques.py:135-138)."""
+    s = np.asarray(sizes, dtype=np.float64)
+    return float((s.sum() ** 2 - (s * s).sum()) / 2.0)
+
+
 def reduce_counts(counts, group=None, device=None):
     import torch
     import torch.distributed as dist

@@ -132,6 +132,41 @@ def test_cli_two_ranks_match_golden(name, tmp_path):
     assert_matches_golden(meta, data, mgs, arrays)
 
 
+def test_bench_self_launch_rank_layout():
+    """`python bench.py --gpus N` with no launcher env spawns N ranks (RANK = LOCAL_RANK = r,
+    WORLD_SIZE = N, rendezvous on 127.0.0.1); a --gpus / WORLD_SIZE mismatch is an error."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3",
+                        "--launch-check"], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = sorted((json.loads(line) for line in r.stdout.strip().splitlines()),
+                 key=lambda d: int(d["RANK"]))
+    assert [(d["RANK"], d["LOCAL_RANK"], d["WORLD_SIZE"], d["MASTER_ADDR"]) for d in got] == \
+        [(str(i), str(i), "3", "127.0.0.1") for i in range(3)]
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4",
+                        "--launch-check"], env=dict(env, WORLD_SIZE="2"), capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+@pytest.mark.gpu
+def test_bench_self_launch_two_ranks():
+    """`python bench.py --gpus 2` with no launcher: two self-spawned ranks (both on cuda:0 over
+    gloo on the 1-GPU test box) report n_gpus 2 and the totals of the 120-micrograph union."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(RGC_BENCH_DEVICE="0", RGC_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--n_mg",
+                        "60", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(s) for s in r.stdout.strip().splitlines() if s.startswith("{")]
+    assert len(lines) == 1
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["totals"]["micrographs"] == 120 and d["value"] > 0
+
+
 @pytest.mark.gpu
 def test_bench_two_ranks_one_gpu():
     """bench.py's sharded path (id-offset all_gather, max-over-ranks timing, counter

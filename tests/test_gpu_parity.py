@@ -189,6 +189,84 @@ def test_gpu_full_c2_properties():
     ctx.close()
 
 
+def _check_vs_vec(mgs, k, box, get_cc=False, no_fused=False, ctx=None):
+    """Every output of the HIP path against the vectorised oracle (oracle/cpu_vec.py, pinned
+    to oracle/cpu_ref.py), bit-exact, at full BASELINE sizes: clique member sets, COO rows,
+    float32 w / conf, consensus box, CC stats."""
+    from oracle import cpu_vec
+    from repic_amd import _lib
+    from repic_amd.pipeline import Batch, run_batch
+    batch = Batch.pack(k, box, mgs)
+    own = ctx is None
+    if own:
+        ctx = _lib.Context(0)
+    res = run_batch(ctx, batch, get_cc=get_cc, no_fused=no_fused, members=True)
+    n_cl = 0
+    for m, mg in enumerate(mgs):
+        b0 = int(batch.box_off[m * k])
+        x, y, s = (np.concatenate([t[i] for t in mg]) for i in range(3))
+        o = cpu_vec.micrograph(x, y, s, [len(t[0]) for t in mg], box, get_cc=get_cc,
+                               id_base=int(batch.id_base[m]))
+        r = res[m]
+        assert o["status"] == "ok" and r.status == _lib.OK
+        assert (r.cc_max, r.cc_cnt) == (o["cc_max"], o["cc_cnt"])
+        assert r.n_edges == o["n_edges"] and r.n_vert == o["V"]
+        mem = r.members.astype(np.int64) - b0
+        assert mem.shape == o["members"].shape, (mem.shape, o["members"].shape)
+        p = np.lexsort(mem.T[::-1])      # oracle members are already lexicographic
+        assert np.array_equal(mem[p], o["members"])
+        assert np.array_equal(r.rows[p], o["rows"])
+        assert np.array_equal(r.w[p].view(np.uint32), o["w"].view(np.uint32))
+        assert np.array_equal(r.conf[p].view(np.uint32), o["conf"].view(np.uint32))
+        assert np.array_equal(r.consensus[p].astype(np.int64) - b0, o["consensus"])
+        n_cl += len(p)
+    if own:
+        ctx.close()
+    return n_cl
+
+
+def _c5_window(mg, x0, y0, W):
+    out = []
+    for (x, y, s) in mg:
+        m = (x >= x0) & (x < x0 + W) & (y >= y0) & (y < y0 + W)
+        out.append((x[m], y[m], s[m]))
+    return out
+
+
+def test_gpu_c5_full_size_matches_vectorised_oracle():
+    """BASELINE config #5 (8 pickers, ~27.5k boxes and ~1M 8-cliques per micrograph, B = 64):
+    two full-size micrographs through the large-micrograph route, every output bit-exact
+    against the vectorised oracle (get_cliques.py:49-56,160-202 clique explosion)."""
+    from repic_amd import synth
+    cfg = synth.SynthConfig(**synth.CONFIGS["C5"], seed=0)
+    mgs = synth.batch(cfg, 2)
+    assert sum(len(t[0]) for t in mgs[0]) > 25000
+    n = _check_vs_vec(mgs, cfg.k, cfg.box)
+    assert n > 1_000_000
+
+
+def test_gpu_c5_windows_match_reference_oracle():
+    """C5 windows small enough for the scalar oracle (pinned to the reference's goldens):
+    768^2 px (~1k boxes, ~7k cliques) and 1024^2 px (~1.8k boxes, ~39k cliques), on the
+    fused route and on the large-micrograph route."""
+    from repic_amd import synth
+    cfg = synth.SynthConfig(**synth.CONFIGS["C5"], seed=0)
+    base = synth.batch(cfg, 2)
+    wins = [_c5_window(base[0], 1000, 1000, 768), _c5_window(base[1], 2500, 300, 768),
+            _c5_window(base[0], 1000, 1000, 1024)]
+    _check_vs_oracle(wins, cfg.k, cfg.box)
+    _check_vs_oracle(wins[:2], cfg.k, cfg.box, no_fused=True)
+
+
+@pytest.mark.parametrize("cfg_name,n_mg,get_cc", [("C3", 16, False), ("C3", 4, True),
+                                                   ("C4", 200, False), ("C2", 400, False)])
+def test_gpu_full_size_configs_match_vectorised_oracle(cfg_name, n_mg, get_cc):
+    """Full-size C2/C3/C4 micrographs (same generator and seed as bench.py), bit-exact."""
+    from repic_amd import synth
+    cfg = synth.SynthConfig(**synth.CONFIGS[cfg_name], seed=0)
+    _check_vs_vec(synth.batch(cfg, n_mg), cfg.k, cfg.box, get_cc=get_cc)
+
+
 def test_gpu_mixed_batch_routes():
     """One batch whose micrographs take every route: f32-layout fused pass, f64 relaunch
     (coordinates not exact in f32), large-LDS relaunch (dense clusters), BFS overflow into
@@ -277,3 +355,35 @@ def _device_meta_check():
         assert all(np.array_equal(u, v) for u, v in zip(ref[f], got[f])), f
     assert sum(len(v) for v in got["w"]) == int(b.n_cliques)
     ctx.close()
+
+
+def test_gpu_cli_end_to_end_subprocess(tmp_path):
+    """`python -m repic_amd.main get_cliques <in> <out> 180` as a separate process (argparse,
+    dispatcher, exit status) on EMPIAR-10017 reproduces the reference's golden outputs."""
+    import json
+    import subprocess
+    import sys
+    name = "c1_10017"
+    meta, data = load_case(name)
+    in_dir = make_inputs(name, str(tmp_path))
+    out_dir = os.path.join(str(tmp_path), "out")
+    lst = os.path.join(str(tmp_path), "listing.json")
+    with open(lst, "w") as f:
+        json.dump(meta["listing"], f)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([os.path.join(root, "repic-copy_amd"),
+                                                       os.environ.get("PYTHONPATH", "")]))
+    r = subprocess.run([sys.executable, "-m", "repic_amd.main", "get_cliques", in_dir, out_dir,
+                        str(meta["box"]), "--listing", lst], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Using crYOLO BOX files as starting point" in r.stdout
+    mgs, arrays = read_outputs(out_dir, meta)
+    assert_matches_golden(meta, data, mgs, arrays)
+    # a crash case exits non-zero with the reference's exception class
+    meta2, _ = load_case("crash_noedges")
+    in2 = make_inputs("crash_noedges", str(tmp_path / "c2"))
+    r = subprocess.run([sys.executable, "-m", "repic_amd.main", "get_cliques", in2,
+                        os.path.join(str(tmp_path), "out2"), str(meta2["box"])], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "ValueError" in r.stderr

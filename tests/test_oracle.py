@@ -65,3 +65,53 @@ def test_jaccard_known_answers():
     inter = xo * yo
     vec = inter / ((2 * B.astype(np.float64) ** 2) - inter)
     assert np.array_equal(vec.view(np.uint64), ji.view(np.uint64))
+
+
+def _vec_vs_ref(mg, box, get_cc=False, idb=1000):
+    """oracle/cpu_vec.py (full-size checker) against oracle/cpu_ref.py, bit-exact."""
+    from oracle import cpu_vec
+    k = len(mg)
+    coords, nid = [], idb
+    for (x, y, s) in mg:
+        coords.append([(float(a), float(b), float(c), nid + i)
+                       for i, (a, b, c) in enumerate(zip(x, y, s))])
+        nid += len(x)
+    o = cpu_ref.micrograph(coords, box, [f"p{i}" for i in range(k)], get_cc=get_cc)
+    X, Y, S = (np.concatenate([m[i] for m in mg]) for i in range(3))
+    v = cpu_vec.micrograph(X, Y, S, [len(m[0]) for m in mg], box, get_cc=get_cc, id_base=idb)
+    A = o["A"].tocoo()
+    C = A.shape[1]
+    orows = np.sort(A.row[np.argsort(A.col, kind="stable")].reshape(C, k), axis=1)
+    po, pv = np.lexsort(orows.T[::-1]), np.lexsort(v["rows"].T[::-1])
+    assert (o["cc_max"], o["cc_cnt"]) == (v["cc_max"], v["cc_cnt"])
+    assert np.array_equal(orows[po], v["rows"][pv])
+    assert np.array_equal(o["w"][po].view(np.uint32), v["w"][pv].view(np.uint32))
+    assert np.array_equal(o["conf"][po].view(np.uint32), v["conf"][pv].view(np.uint32))
+    got = [(float(X[g]), float(Y[g]), idb + int(g)) for g in v["consensus"][pv]]
+    assert got == [o["consensus"][i] for i in po]
+    return C
+
+
+@pytest.mark.parametrize("cfg_name,n,extra", [
+    ("C2", 3, {}), ("C2", 2, {"frac": True, "dup": 0.2}), ("C4", 2, {"logit": (1,)}),
+    ("C3", 1, {})])
+def test_vectorised_oracle_matches_scalar(cfg_name, n, extra):
+    from repic_amd import synth
+    from repic_amd.ingest import sigmoid
+    cfg = synth.SynthConfig(**{**synth.CONFIGS[cfg_name], **extra}, seed=5)
+    for mg in synth.batch(cfg, n):
+        mg = [(x, y, sigmoid(s) if s.min() < 0 else s) for (x, y, s) in mg]
+        assert _vec_vs_ref(mg, cfg.box) > 0
+        _vec_vs_ref(mg, cfg.box, get_cc=True)
+
+
+def test_vectorised_oracle_matches_scalar_c5_window():
+    """A 768^2 window of a full C5 micrograph (k = 8, duplicates -> degree ties)."""
+    from repic_amd import synth
+    cfg = synth.SynthConfig(**synth.CONFIGS["C5"], seed=0)
+    mg = synth.batch(cfg, 1)[0]
+    win = []
+    for (x, y, s) in mg:
+        m = (x >= 1000) & (x < 1768) & (y >= 1000) & (y < 1768)
+        win.append((x[m], y[m], s[m]))
+    assert _vec_vs_ref(win, cfg.box) > 5000
