@@ -56,7 +56,7 @@ enum DevBufId {
   D_ROWS, D_W, D_CONF, D_CONS, D_MEMBERS, D_ORDER,
   // multi-kernel path (sub-batch)
   D_SUBMG, D_SUBX, D_SUBY, D_SUBS, D_ORIG, D_STAMPS,
-  D_BOXOFF, D_CELLOFF, D_IDBASE, D_GRID, D_CELLSTART, D_SX, D_SY, D_SBOX, D_SPICK, D_SMG, D_BMG,
+  D_BOXOFF, D_CELLOFF, D_P0OFF, D_IDBASE, D_GRID, D_CELLSTART, D_SX, D_SY, D_SBOX, D_SPICK, D_SMG, D_BMG,
   D_BPICK, D_FWDCNT, D_FWDOFF, D_TILES, D_TOTAL, D_EDST, D_EJI, D_PARENT, D_HASEDGE, D_CSIZE,
   D_STAT, D_INSKEY, D_COMPMIN, D_CCOUNT, D_COFF, D_INCL, D_VLIST, D_VSORT, D_VROW, D_MGOFF,
   // RGC_F_EDGES test hook
@@ -251,18 +251,26 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   }
   cell_off[n_mg] = (int32_t)cells;
   if (cells >= (1LL << 31)) return fail("too many grid cells in one batch");
-  const size_t stage_bytes = nbo * 4 + (n_mg + 1) * 4 + n_mg * 8 + 64;
+  const size_t stage_bytes = nbo * 4 + 2 * (n_mg + 1) * 4 + n_mg * 8 + 64;
   TRY(ensure_host(c, H_STAGE, stage_bytes));
   int32_t* st_bo = H<int32_t>(c, H_STAGE);
   int32_t* st_co = st_bo + nbo;
+  int32_t* st_p0 = st_co + n_mg + 1;   // picker-0 prefix: wavefront -> clique root
   int64_t* st_id = reinterpret_cast<int64_t*>(
-      (reinterpret_cast<uintptr_t>(st_co + n_mg + 1) + 7) & ~(uintptr_t)7);
+      (reinterpret_cast<uintptr_t>(st_p0 + n_mg + 1) + 7) & ~(uintptr_t)7);
   for (size_t i = 0; i < nbo; ++i) st_bo[i] = (int32_t)box_off[i];
   std::memcpy(st_co, cell_off.data(), (n_mg + 1) * 4);
   std::memcpy(st_id, id_base, n_mg * 8);
+  int64_t n_roots = 0;
+  for (int m = 0; m < n_mg; ++m) {
+    st_p0[m] = (int32_t)n_roots;
+    n_roots += box_off[(int64_t)m * k + 1] - box_off[(int64_t)m * k];
+  }
+  st_p0[n_mg] = (int32_t)n_roots;
 
   TRY(ensure_dev(c, D_BOXOFF, nbo * 4));
   TRY(ensure_dev(c, D_CELLOFF, (n_mg + 1) * 4));
+  TRY(ensure_dev(c, D_P0OFF, (n_mg + 1) * 4));
   TRY(ensure_dev(c, D_IDBASE, n_mg * 8));
   TRY(ensure_dev(c, D_GRID, n_mg * sizeof(MgGrid)));
   TRY(ensure_dev(c, D_CELLSTART, cells * 4));
@@ -298,11 +306,13 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   TRY(mark(c, "h2d_meta"));
   HIPCHK(hipMemcpyAsync(D<void>(c, D_BOXOFF), st_bo, nbo * 4, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(D<void>(c, D_CELLOFF), st_co, (n_mg + 1) * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(D<void>(c, D_P0OFF), st_p0, (n_mg + 1) * 4, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(D<void>(c, D_IDBASE), st_id, n_mg * 8, hipMemcpyHostToDevice, s));
   TRY(mark(c, "memset"));
   HIPCHK(hipMemsetAsync(D<void>(c, D_HASEDGE), 0, N, s));
   HIPCHK(hipMemsetAsync(D<void>(c, D_CSIZE), 0, N * 4, s));
   HIPCHK(hipMemsetAsync(D<void>(c, D_INCL), 0, N, s));
+  HIPCHK(hipMemsetAsync(D<void>(c, D_CCOUNT), 0, N * 4, s));
   HIPCHK(hipMemsetAsync(D<void>(c, D_INSKEY), 0xff, N * 8, s));
   if (get_cc) HIPCHK(hipMemsetAsync(D<void>(c, D_COMPMIN), 0xff, N * 8, s));
 
@@ -346,38 +356,46 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
               D<unsigned long long>(c, D_INSKEY), D<unsigned long long>(c, D_COMPMIN));
   }
 
-  CliqueArgsHost A;
-  A.k = k; A.flags = get_cc | (multi << 1); A.box_off = bo; A.id_base = D<int64_t>(c, D_IDBASE);
+  CliqueArgs A;
+  A.k = k; A.flags = get_cc | (multi << 1); A.n_mg = n_mg; A.n_roots = n_roots; A.C = 0;
+  A.B = B; A.two_b2 = two_b2;
+  A.box_off = bo; A.p0off = D<int32_t>(c, D_P0OFF); A.id_base = D<int64_t>(c, D_IDBASE);
   A.x = x; A.y = y; A.score = sc; A.bmg = D<int32_t>(c, D_BMG); A.bpick = D<uint8_t>(c, D_BPICK);
-  A.fwd_off = D<int64_t>(c, D_FWDOFF); A.e_dst = D<int32_t>(c, D_EDST); A.e_ji = D<double>(c, D_EJI);
+  A.fwd_off = D<int64_t>(c, D_FWDOFF); A.e_dst = D<int32_t>(c, D_EDST);
   A.parent = D<int32_t>(c, D_PARENT); A.st = D<MgStat>(c, D_STAT);
   A.ins_key = D<unsigned long long>(c, D_INSKEY); A.clique_off = D<int64_t>(c, D_COFF);
+  A.vrow = D<int32_t>(c, D_VROW);
   A.ccount = D<int32_t>(c, D_CCOUNT); A.in_clique = D<uint8_t>(c, D_INCL);
-  A.members = nullptr; A.w = nullptr; A.conf = nullptr; A.consensus = nullptr; A.order = nullptr;
+  A.members = nullptr; A.rows = nullptr; A.w = nullptr; A.conf = nullptr; A.consensus = nullptr;
+  A.order = nullptr;
   TRY(mark(c, "k5_cliques_count"));
-  if (launch_cliques(s, false, (int)N, A) != 0) return fail("unsupported k");
+  if (launch_cliques(s, 0, (int)N, A) != 0) return fail("unsupported k");
   TRY(mark(c, "scan_cliques"));
   launch_scan(s, N, D<int32_t>(c, D_CCOUNT), D<int64_t>(c, D_COFF), D<int64_t>(c, D_TILES),
               D<int64_t>(c, D_TOTAL));
   HIPCHK(hipMemcpyAsync(H<int64_t>(c, H_TOTAL), D<int64_t>(c, D_TOTAL), 8,
                         hipMemcpyDeviceToHost, s));
+  // row ranks need only the clique-vertex flags of the count pass: overlap with the host's
+  // read of the total
+  TRY(mark(c, "k7_rank"));
+  launch_rank(s, n_mg, k, bo, x, y, D<uint8_t>(c, D_INCL), D<int32_t>(c, D_VLIST),
+              D<int32_t>(c, D_VSORT), D<int32_t>(c, D_VROW), D<MgStat>(c, D_STAT));
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
   const int64_t C = H<int64_t>(c, H_TOTAL)[0];
   *C_out = C;
   TRY(ensure_outputs(c, out_base + C, out_base, k, true, multi != 0));
+  A.C = C;
   A.members = D<int32_t>(c, D_MEMBERS) + out_base * k;
+  A.rows = D<int32_t>(c, D_ROWS) + out_base * k;
   A.w = D<float>(c, D_W) + out_base;
   A.conf = D<float>(c, D_CONF) + out_base;
   A.consensus = D<int32_t>(c, D_CONS) + out_base;
   A.order = multi ? D<uint8_t>(c, D_ORDER) + out_base * k : nullptr;
   TRY(mark(c, "k5_cliques_fill"));
-  launch_cliques(s, true, (int)N, A);
-  TRY(mark(c, "k7_rank"));
-  launch_rank(s, n_mg, k, bo, x, y, D<uint8_t>(c, D_INCL), D<int32_t>(c, D_VLIST),
-              D<int32_t>(c, D_VSORT), D<int32_t>(c, D_VROW), D<MgStat>(c, D_STAT));
-  TRY(mark(c, "k7_rows"));
-  launch_rows(s, k, C, A.members, D<int32_t>(c, D_VROW), D<int32_t>(c, D_ROWS) + out_base * k);
+  launch_cliques(s, 1, (int)N, A);
+  TRY(mark(c, "k5_epilogue"));
+  launch_cliques(s, 2, (int)N, A);
   TRY(mark(c, "k_mg_offsets"));
   launch_mg_offsets(s, n_mg, k, bo, D<int64_t>(c, D_COFF), D<int64_t>(c, D_MGOFF));
   HIPCHK(hipMemcpyAsync(H<void>(c, H_STAT), D<void>(c, D_STAT), n_mg * sizeof(MgStat),

@@ -105,10 +105,18 @@ void launch_dump_edges(hipStream_t stream, int N, const int64_t* fwd_off, const 
                        const double* e_ji, const int32_t* orig, int32_t* eu, int32_t* ev,
                        double* eji);
 
-struct CliqueArgsHost {
+// Clique stage of the large-micrograph route (rgc_cliques.hip + the DFS fallback in
+// rgc_kernels.hip).  Boxes are sub-batch indices; outputs are offset by the caller.
+constexpr int RB_W = 64;   // bitmap width: roots with <= RB_W forward neighbours use a wavefront
+
+struct CliqueArgs {
   int k;
   int flags;                 // bit 0: --get_cc, bit 1: --multi_out
+  int n_mg, n_roots;         // micrographs; picker-0 boxes (one wavefront each)
+  int64_t C;                 // epilogue: cliques of the sub-batch
+  double B, two_b2;          // box size, 2 B^2
   const int32_t* box_off;
+  const int32_t* p0off;      // [n_mg + 1] exclusive prefix of picker-0 box counts
   const int64_t* id_base;
   const double* x;
   const double* y;
@@ -117,19 +125,21 @@ struct CliqueArgsHost {
   const uint8_t* bpick;
   const int64_t* fwd_off;
   const int32_t* e_dst;
-  const double* e_ji;
   const int32_t* parent;
   const MgStat* st;
   const unsigned long long* ins_key;
   const int64_t* clique_off;
+  const int32_t* vrow;
   int32_t* ccount;
+  uint8_t* in_clique;
   int32_t* members;
+  int32_t* rows;
   float* w;
   float* conf;
   int32_t* consensus;
   uint8_t* order;
-  uint8_t* in_clique;
 };
+
 
 void launch_bin(hipStream_t stream, int n_mg, int k, double B, const int32_t* box_off,
                 const int32_t* cell_off, const double* x, const double* y, MgGrid* grid,
@@ -148,12 +158,12 @@ void launch_cc(hipStream_t stream, int phase, int N, int n_mg, int k, int get_cc
                const int64_t* fwd_off, const int32_t* e_dst, int32_t* parent, uint8_t* has_edge,
                int32_t* csize, MgStat* st, unsigned long long* ins_key,
                unsigned long long* comp_min);
-int launch_cliques(hipStream_t stream, bool fill, int N, const CliqueArgsHost& h);
+// phase 0: count cliques per root + mark clique vertices; 1: write members; 2: ILP epilogue
+int launch_cliques(hipStream_t stream, int phase, int N, const CliqueArgs& A);
+int launch_cliques_dfs(hipStream_t stream, bool fill, int N, const CliqueArgs& A);
 void launch_rank(hipStream_t stream, int n_mg, int k, const int32_t* box_off, const double* x,
                  const double* y, const uint8_t* in_clique, int32_t* vlist, int32_t* vsort,
                  int32_t* vrow, MgStat* st);
-int launch_rows(hipStream_t stream, int k, int64_t C, const int32_t* members,
-                const int32_t* vrow, int32_t* rows);
 void launch_mg_offsets(hipStream_t stream, int n_mg, int k, const int32_t* box_off,
                        const int64_t* coff, int64_t* mg_off);
 

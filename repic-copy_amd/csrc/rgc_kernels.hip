@@ -7,12 +7,11 @@
 //   k2_pairs<FILL>    calc_jaccard (:40-46) + |dx| <= B prefilter + JI > 0.3 (:64-65,:138),
 //                     two-phase count -> scan -> fill; forward CSR sorted by target box
 //   k4_*              nx.connected_components stats (:145-149), --get_cc (:151-156)
-//   k5_cliques<K,..>  find_cliques (:49-56) as one-box-per-picker k-tuple enumeration by
-//                     sorted neighbour-list intersection, fused with the ILP epilogue
-//                     (:169-190): conf, w, weighted degree, consensus with the CPython
-//                     set-order tie-break (pyset.h)
-//   k7_rank/k7_rows   row index v.index() (:164,:193) as a per-micrograph rank by
-//                     (x, y, id); COO rows (:192-202)
+//   k5_cliques<K,..>  find_cliques (:49-56) for roots with more than RB_W forward
+//                     neighbours (the wavefront bitmap kernels of rgc_cliques.hip take the
+//                     rest; the ILP epilogue is k5_epilogue there)
+//   k7_rank           row index v.index() (:164,:193) as a per-micrograph rank by
+//                     (x, y, id)
 //
 // Floating point: every JI / degree / median operation keeps the reference's f64 operation
 // order; contraction into FMA is forbidden (the pragma below + -ffp-contract=off).
@@ -418,33 +417,13 @@ __global__ __launch_bounds__(WG) void k4_target(int k, const int32_t* __restrict
   }
 }
 
-// ----------------------------------------------------------------------------- K5 cliques
-struct CliqueArgs {
-  int k;
-  int flags;
-  const int32_t* box_off;
-  const int64_t* id_base;
-  const double* x;
-  const double* y;
-  const double* score;
-  const int32_t* bmg;
-  const uint8_t* bpick;
-  const int64_t* fwd_off;
-  const int32_t* e_dst;
-  const double* e_ji;
-  const int32_t* parent;
-  const MgStat* st;
-  const unsigned long long* ins_key;
-  const int64_t* clique_off;
-  int32_t* ccount;
-  int32_t* members;
-  float* w;
-  float* conf;
-  int32_t* consensus;
-  uint8_t* order;
-  uint8_t* in_clique;
-};
-
+// ----------------------------------------------------------------------------- K5 fallback
+// Roots whose forward neighbourhood exceeds the bitmap width of the wavefront kernels
+// (rgc_cliques.hip, RB_W boxes) are enumerated here, one thread per root, depth-first over the
+// global forward CSR (sorted-list membership by binary search).  COUNT: cliques per root and
+// the clique-vertex flags; FILL: the members of each clique at the root's scanned offset (the
+// ILP epilogue is the shared thread-per-clique kernel).  Lexicographic order, like the
+// wavefront kernels.
 __device__ __forceinline__ int64_t lower_bound(const int32_t* a, int64_t lo, int64_t hi, int v) {
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
@@ -456,57 +435,11 @@ __device__ __forceinline__ int64_t lower_bound(const int32_t* a, int64_t lo, int
 template <int K>
 struct Walk {
   int mem[K];        // chosen box per picker
-  double ji[K][K];   // ji[i][j], i < j
   int pb[K + 1];     // picker box bounds of this micrograph
   int64_t count;
   int64_t out;       // next output clique index (FILL)
-  int m;
 };
 
-template <int K>
-__device__ void emit_clique(const CliqueArgs& A, Walk<K>& W) {
-  const int64_t j = W.out++;
-  const int m = W.m;
-  double s[K], xs[K], ys[K];
-  int64_t ids[K];
-  uint64_t ins[K] = {};
-  const int64_t idb = A.id_base[m] - (int64_t)A.box_off[m * A.k];
-#pragma unroll
-  for (int i = 0; i < K; ++i) {
-    const int g = W.mem[i];
-    s[i] = A.score[g];
-    xs[i] = A.x[g];
-    ys[i] = A.y[g];
-    ids[i] = idb + g;
-  }
-  const bool multi = (A.flags & 2) != 0;
-  const bool set_order = 2 * K < A.st[m].n_nodes;
-  if (!set_order) {
-#pragma unroll
-    for (int i = 0; i < K; ++i) ins[i] = A.ins_key[W.mem[i]];
-  }
-  Epi<K> e;
-  epilogue<K>(W.mem, W.ji, s, xs, ys, ids, set_order, ins, multi, e);
-  A.w[j] = e.w;
-  A.conf[j] = e.conf;
-  int cons = W.mem[0];
-#pragma unroll
-  for (int i = 1; i < K; ++i) cons = (e.arg == i) ? W.mem[i] : cons;
-  A.consensus[j] = cons;
-#pragma unroll
-  for (int i = 0; i < K; ++i) {
-    A.members[j * K + i] = W.mem[i];
-    A.in_clique[W.mem[i]] = 1;
-  }
-  if (multi) {
-    for (int i = 0; i < K; ++i) A.order[j * K + i] = (uint8_t)e.ord[i];
-  }
-}
-
-// Depth-first enumeration: level D chooses the picker-D member among the forward
-// neighbours of the picker-(D-1) member that are also forward neighbours of every earlier
-// member (sorted-list intersection by binary search).  Static recursion keeps every
-// per-level value in registers.
 template <int K, int D, bool FILL>
 struct Level {
   __device__ static void run(const CliqueArgs& A, Walk<K>& W) {
@@ -524,11 +457,9 @@ struct Level {
         const int64_t c0 = A.fwd_off[c], c1 = A.fwd_off[c + 1];
         const int64_t pos = lower_bound(A.e_dst, c0, c1, h);
         if (pos >= c1 || A.e_dst[pos] != h) { ok = false; break; }
-        if (FILL) W.ji[q][D] = A.e_ji[pos];
       }
       if (!ok) continue;
       W.mem[D] = h;
-      if (FILL) W.ji[D - 1][D] = A.e_ji[e];
       Level<K, D + 1, FILL>::run(A, W);
     }
   }
@@ -536,8 +467,15 @@ struct Level {
 template <int K, bool FILL>
 struct Level<K, K, FILL> {
   __device__ static void run(const CliqueArgs& A, Walk<K>& W) {
-    if (FILL) emit_clique<K>(A, W);
-    else ++W.count;
+    if (FILL) {
+      const int64_t j = W.out++;
+#pragma unroll
+      for (int i = 0; i < K; ++i) A.members[j * K + i] = W.mem[i];
+    } else {
+      ++W.count;
+#pragma unroll
+      for (int i = 0; i < K; ++i) A.in_clique[W.mem[i]] = 1;
+    }
   }
 };
 
@@ -545,19 +483,14 @@ template <int K, bool FILL>
 __global__ __launch_bounds__(WG) void k5_cliques(int N, CliqueArgs A) {
   const int g = blockIdx.x * WG + threadIdx.x;
   if (g >= N) return;
-  bool root = A.bpick[g] == 0 && A.fwd_off[g] != A.fwd_off[g + 1];
-  const int m = root ? A.bmg[g] : 0;
-  if (root) {
-    const MgStat s = A.st[m];
-    if (s.status != 0) root = false;
-    if ((A.flags & 1) && A.parent[g] != s.target) root = false;
-  }
-  if (!root) {
-    if (!FILL) A.ccount[g] = 0;
-    return;
-  }
+  if (A.bpick[g] != 0) return;
+  const int64_t d = A.fwd_off[g + 1] - A.fwd_off[g];
+  if (d <= RB_W) return;   // the wavefront kernels' root
+  const int m = A.bmg[g];
+  const MgStat s = A.st[m];
+  if (s.status != 0) return;
+  if ((A.flags & 1) && A.parent[g] != s.target) return;
   Walk<K> W;
-  W.m = m;
   W.count = 0;
   W.out = FILL ? A.clique_off[g] : 0;
 #pragma unroll
@@ -643,24 +576,6 @@ __global__ __launch_bounds__(WG) void k7_rank(int k, const int32_t* __restrict__
     }
     vrow[g] = r;
   }
-}
-
-template <int K>
-__global__ __launch_bounds__(WG) void k7_rows(int64_t C, const int32_t* __restrict__ members,
-                                              const int32_t* __restrict__ vrow, int32_t* rows) {
-  const int64_t j = (int64_t)blockIdx.x * WG + threadIdx.x;
-  if (j >= C) return;
-  int r[K];
-#pragma unroll
-  for (int i = 0; i < K; ++i) r[i] = vrow[members[j * K + i]];
-  for (int i = 1; i < K; ++i) {
-    const int t = r[i];
-    int q = i - 1;
-    while (q >= 0 && r[q] > t) { r[q + 1] = r[q]; --q; }
-    r[q + 1] = t;
-  }
-#pragma unroll
-  for (int i = 0; i < K; ++i) rows[j * K + i] = r[i];
 }
 
 __global__ __launch_bounds__(WG) void k_mg_offsets(int n_mg, int k, const int32_t* __restrict__ box_off,
@@ -797,28 +712,22 @@ void launch_cc(hipStream_t stream, int phase, int N, int n_mg, int k, int get_cc
 }
 
 template <int K>
-static void launch_cliques_k(hipStream_t stream, bool fill, int N, const CliqueArgsHost& h) {
-  CliqueArgs A;
-  A.k = h.k; A.flags = h.flags; A.box_off = h.box_off; A.id_base = h.id_base; A.x = h.x;
-  A.y = h.y; A.score = h.score; A.bmg = h.bmg; A.bpick = h.bpick; A.fwd_off = h.fwd_off;
-  A.e_dst = h.e_dst; A.e_ji = h.e_ji; A.parent = h.parent; A.st = h.st; A.ins_key = h.ins_key;
-  A.clique_off = h.clique_off; A.ccount = h.ccount; A.members = h.members; A.w = h.w;
-  A.conf = h.conf; A.consensus = h.consensus; A.order = h.order; A.in_clique = h.in_clique;
+static void launch_dfs_k(hipStream_t stream, bool fill, int N, const CliqueArgs& A) {
   const int nb = (N + WG - 1) / WG;
   if (!nb) return;
   if (fill) RGC_LAUNCH((k5_cliques<K, true>), nb, WG, N, A);
   else RGC_LAUNCH((k5_cliques<K, false>), nb, WG, N, A);
 }
 
-int launch_cliques(hipStream_t stream, bool fill, int N, const CliqueArgsHost& h) {
-  switch (h.k) {
-    case 2: launch_cliques_k<2>(stream, fill, N, h); break;
-    case 3: launch_cliques_k<3>(stream, fill, N, h); break;
-    case 4: launch_cliques_k<4>(stream, fill, N, h); break;
-    case 5: launch_cliques_k<5>(stream, fill, N, h); break;
-    case 6: launch_cliques_k<6>(stream, fill, N, h); break;
-    case 7: launch_cliques_k<7>(stream, fill, N, h); break;
-    case 8: launch_cliques_k<8>(stream, fill, N, h); break;
+int launch_cliques_dfs(hipStream_t stream, bool fill, int N, const CliqueArgs& A) {
+  switch (A.k) {
+    case 2: launch_dfs_k<2>(stream, fill, N, A); break;
+    case 3: launch_dfs_k<3>(stream, fill, N, A); break;
+    case 4: launch_dfs_k<4>(stream, fill, N, A); break;
+    case 5: launch_dfs_k<5>(stream, fill, N, A); break;
+    case 6: launch_dfs_k<6>(stream, fill, N, A); break;
+    case 7: launch_dfs_k<7>(stream, fill, N, A); break;
+    case 8: launch_dfs_k<8>(stream, fill, N, A); break;
     default: return -1;
   }
   return 0;
@@ -828,23 +737,6 @@ void launch_rank(hipStream_t stream, int n_mg, int k, const int32_t* box_off, co
                  const double* y, const uint8_t* in_clique, int32_t* vlist, int32_t* vsort,
                  int32_t* vrow, MgStat* st) {
   RGC_LAUNCH(k7_rank, n_mg, WG, k, box_off, x, y, in_clique, vlist, vsort, vrow, st);
-}
-
-int launch_rows(hipStream_t stream, int k, int64_t C, const int32_t* members,
-                const int32_t* vrow, int32_t* rows) {
-  const int64_t nb = (C + WG - 1) / WG;
-  if (!nb) return 0;
-  switch (k) {
-    case 2: RGC_LAUNCH(k7_rows<2>, nb, WG, C, members, vrow, rows); break;
-    case 3: RGC_LAUNCH(k7_rows<3>, nb, WG, C, members, vrow, rows); break;
-    case 4: RGC_LAUNCH(k7_rows<4>, nb, WG, C, members, vrow, rows); break;
-    case 5: RGC_LAUNCH(k7_rows<5>, nb, WG, C, members, vrow, rows); break;
-    case 6: RGC_LAUNCH(k7_rows<6>, nb, WG, C, members, vrow, rows); break;
-    case 7: RGC_LAUNCH(k7_rows<7>, nb, WG, C, members, vrow, rows); break;
-    case 8: RGC_LAUNCH(k7_rows<8>, nb, WG, C, members, vrow, rows); break;
-    default: return -1;
-  }
-  return 0;
 }
 
 void launch_mg_offsets(hipStream_t stream, int n_mg, int k, const int32_t* box_off,
