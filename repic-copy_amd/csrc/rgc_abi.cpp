@@ -58,7 +58,7 @@ enum DevBufId {
   D_SUBMG, D_SUBX, D_SUBY, D_SUBS, D_ORIG, D_STAMPS,
   D_BOXOFF, D_CELLOFF, D_P0OFF, D_IDBASE, D_GRID, D_CELLSTART, D_SX, D_SY, D_SBOX, D_SPICK, D_SMG, D_BMG,
   D_BPICK, D_FWDCNT, D_FWDOFF, D_TILES, D_TOTAL, D_EDST, D_EJI, D_PARENT, D_HASEDGE, D_CSIZE,
-  D_STAT, D_INSKEY, D_COMPMIN, D_CCOUNT, D_COFF, D_INCL, D_VLIST, D_VSORT, D_VROW, D_MGOFF,
+  D_STAT, D_INSKEY, D_COMPMIN, D_CCOUNT, D_COFF, D_INCL, D_VLIST, D_VSORT, D_VROW, D_BOFF, D_MGOFF,
   // RGC_F_EDGES test hook
   D_EU, D_EV, D_EJIOUT,
   D_COUNT
@@ -297,6 +297,7 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   TRY(ensure_dev(c, D_VLIST, N * 4));
   TRY(ensure_dev(c, D_VSORT, N * 4));
   TRY(ensure_dev(c, D_VROW, N * 4));
+  TRY(ensure_dev(c, D_BOFF, (N + 1) * 8));
   TRY(ensure_dev(c, D_MGOFF, (n_mg + 1) * 8));
   TRY(ensure_host(c, H_TOTAL, 16));
   TRY(ensure_host(c, H_STAT, n_mg * sizeof(MgStat)));
@@ -313,6 +314,7 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   HIPCHK(hipMemsetAsync(D<void>(c, D_CSIZE), 0, N * 4, s));
   HIPCHK(hipMemsetAsync(D<void>(c, D_INCL), 0, N, s));
   HIPCHK(hipMemsetAsync(D<void>(c, D_CCOUNT), 0, N * 4, s));
+  HIPCHK(hipMemsetAsync(D<void>(c, D_VLIST), 0, N * 4, s));   // row-rank bucket counters
   HIPCHK(hipMemsetAsync(D<void>(c, D_INSKEY), 0xff, N * 8, s));
   if (get_cc) HIPCHK(hipMemsetAsync(D<void>(c, D_COMPMIN), 0xff, N * 8, s));
 
@@ -375,10 +377,13 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
               D<int64_t>(c, D_TOTAL));
   HIPCHK(hipMemcpyAsync(H<int64_t>(c, H_TOTAL), D<int64_t>(c, D_TOTAL), 8,
                         hipMemcpyDeviceToHost, s));
-  // row ranks need only the clique-vertex flags of the count pass: overlap with the host's
-  // read of the total
+  // row ranks need only the clique-vertex flags of the count pass: queued before the host
+  // waits for the clique total (bucket counters in D_VLIST, slots in D_CSIZE: the CC sizes
+  // are dead by now; the scan total goes to the second D_TOTAL slot)
   TRY(mark(c, "k7_rank"));
-  launch_rank(s, n_mg, k, bo, x, y, D<uint8_t>(c, D_INCL), D<int32_t>(c, D_VLIST),
+  launch_rank(s, (int)N, n_mg, k, bo, D<int32_t>(c, D_BMG), D<MgGrid>(c, D_GRID), x, y,
+              D<uint8_t>(c, D_INCL), D<int32_t>(c, D_VLIST), D<int32_t>(c, D_CSIZE),
+              D<int64_t>(c, D_BOFF), D<int64_t>(c, D_TILES), D<int64_t>(c, D_TOTAL) + 1,
               D<int32_t>(c, D_VSORT), D<int32_t>(c, D_VROW), D<MgStat>(c, D_STAT));
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));

@@ -63,17 +63,34 @@ __device__ __forceinline__ RootInfo root_info(const CliqueArgs& A, int w) {
   return R;
 }
 
-// neighbourhood of the root in LDS: nb[i] = i-th forward neighbour, adj[i] = bitmask of the
-// neighbourhood members adjacent to it (forward edges only: higher pickers); pm[p] = lanes
-// holding picker-p boxes
+constexpr int ECAP = 64;            // prefixes per level buffer (per wavefront)
+
+// A prefix of a root's clique: members for pickers 1..D as neighbourhood lanes (6 bits each,
+// picker q at bits 6(q-1)) and the mask of neighbourhood lanes adjacent to all of them.
+struct Ent {
+  uint64_t M;
+  uint64_t P;
+};
+
+// per-wavefront LDS
+template <int K>
+struct WaveLds {
+  int32_t nb[RB_W];           // neighbourhood (forward neighbours of the root), sorted
+  uint64_t adj[RB_W];         // adj[i]: neighbourhood lanes adjacent to lane i (forward)
+  uint64_t pm[K];             // pm[p]: neighbourhood lanes of picker p
+  Ent buf[K - 1][ECAP];       // level D prefixes (D = 0..K-2; level 0 = the root alone)
+  uint32_t sc[ECAP];          // fill: inclusive scan of the leaf counts of the leaf level
+};
+
+// neighbourhood of the root: nb, adj, pm
 template <int K>
 __device__ __forceinline__ void neighbourhood(const CliqueArgs& A, const RootInfo& R, int lane,
-                                              int32_t* nb, uint64_t* adj, uint64_t (&pm)[K]) {
+                                              WaveLds<K>& L) {
   int u = -1, pk = -1;
   if (lane < R.d) {
     u = A.e_dst[R.lo + lane];
     pk = A.bpick[u];
-    nb[lane] = u;
+    L.nb[lane] = u;
   }
   wave_sync();
   uint64_t mask = 0;
@@ -82,7 +99,7 @@ __device__ __forceinline__ void neighbourhood(const CliqueArgs& A, const RootInf
     int64_t e = A.fwd_off[u];
     const int64_t e1 = A.fwd_off[u + 1];
     int j = lane + 1;
-    int v = j < R.d ? nb[j] : 0;
+    int v = j < R.d ? L.nb[j] : 0;
     while (e < e1 && j < R.d) {
       const int t = A.e_dst[e];
       if (t < v) {
@@ -90,77 +107,26 @@ __device__ __forceinline__ void neighbourhood(const CliqueArgs& A, const RootInf
       } else {
         if (t == v) { mask |= 1ull << j; ++e; }
         ++j;
-        v = j < R.d ? nb[j] : 0;
+        v = j < R.d ? L.nb[j] : 0;
       }
     }
   }
-  adj[lane] = mask;
-  pm[0] = 0;
+  L.adj[lane] = mask;
 #pragma unroll
-  for (int p = 1; p < K; ++p) pm[p] = __ballot(pk == p);
+  for (int p = 0; p < K; ++p) {
+    const uint64_t b = __ballot(pk == p);
+    if (lane == 0) L.pm[p] = b;
+  }
   wave_sync();
 }
 
-// cliques below a prefix whose common-neighbour mask is M, choosing pickers D..K-1
-template <int K, int D>
-struct BCount {
-  __device__ __forceinline__ static uint32_t run(const uint64_t* adj, const uint64_t (&pm)[K],
-                                                 uint64_t M, uint64_t& used) {
-    if constexpr (D == K - 1) {
-      const uint64_t c = M & pm[D];
-      used |= c;
-      return (uint32_t)__popcll(c);
-    } else {
-      uint64_t c = M & pm[D];
-      uint32_t tot = 0;
-      while (c) {
-        const int v = __builtin_ctzll(c);
-        c &= c - 1;
-        const uint32_t n = BCount<K, D + 1>::run(adj, pm, M & adj[v], used);
-        if (n) {
-          used |= 1ull << v;
-          tot += n;
-        }
-      }
-      return tot;
-    }
-  }
-};
-
-template <int K, int D>
-struct BFill {
-  __device__ __forceinline__ static void run(const uint64_t* adj, const int32_t* nb,
-                                             const uint64_t (&pm)[K], uint64_t M, int (&mem)[K],
-                                             int32_t* out, int64_t& j) {
-    uint64_t c = M & pm[D];
-    while (c) {
-      const int v = __builtin_ctzll(c);
-      c &= c - 1;
-      mem[D] = nb[v];
-      if constexpr (D == K - 1) {
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
 #pragma unroll
-        for (int i = 0; i < K; ++i) out[j * K + i] = mem[i];
-        ++j;
-      } else {
-        BFill<K, D + 1>::run(adj, nb, pm, M & adj[v], mem, out, j);
-      }
-    }
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
   }
-};
-
-// cliques whose picker-1 member is this lane's neighbour (0 if it is not a picker-1 box)
-template <int K>
-__device__ __forceinline__ uint32_t lane_count(const uint64_t* adj, const uint64_t (&pm)[K],
-                                               int lane, uint64_t& used) {
-  if (!((pm[1] >> lane) & 1)) return 0;
-  uint32_t n;
-  if constexpr (K == 2) {
-    n = 1;
-  } else {
-    n = BCount<K, 2>::run(adj, pm, adj[lane], used);
-  }
-  if (n) used |= 1ull << lane;
-  return n;
+  return v;
 }
 
 __device__ __forceinline__ uint64_t wave_or(uint64_t v) {
@@ -169,63 +135,200 @@ __device__ __forceinline__ uint64_t wave_or(uint64_t v) {
   return v;
 }
 
+// Expand level-D prefixes, from *cur on, into the (empty) level D+1 buffer until it is full.
+// A child is kept only if it can still be completed (it has a candidate in picker D+2).
+// Wave-cooperative: one prefix per lane, children placed by a wave scan; whole prefixes
+// only, in order, so level D+1 stays lexicographic.  Returns the children written.
+template <int K>
+__device__ int expand(WaveLds<K>& L, int D, int& cur, int n_src, int lane) {
+  const uint64_t pnext = L.pm[D + 1];
+  const uint64_t pafter = D + 2 < K ? L.pm[D + 2] : ~0ull;
+  Ent* src = L.buf[D];
+  Ent* dst = L.buf[D + 1];
+  int nd = 0;
+  while (cur < n_src && nd < ECAP) {
+    const int e = cur + lane;
+    Ent x = {0, 0};
+    uint32_t cnt = 0;
+    if (e < n_src) {
+      x = src[e];
+      uint64_t c = x.M & pnext;
+      while (c) {
+        const int v = __builtin_ctzll(c);
+        c &= c - 1;
+        cnt += (x.M & L.adj[v] & pafter) ? 1u : 0u;
+      }
+    }
+    const uint32_t inc = wave_incl_scan(cnt, lane);
+    const bool ok = e < n_src && (int)inc <= ECAP - nd;
+    const int nacc = __popcll(__ballot(ok));
+    if (ok && cnt) {
+      int o = nd + (int)(inc - cnt);
+      uint64_t c = x.M & pnext;
+      while (c) {
+        const int v = __builtin_ctzll(c);
+        c &= c - 1;
+        const uint64_t m2 = x.M & L.adj[v];
+        if (m2 & pafter) {
+          Ent y;
+          y.M = m2;
+          y.P = x.P | ((uint64_t)v << (6 * D));
+          dst[o++] = y;
+        }
+      }
+    }
+    if (nacc == 0) break;   // the next prefix's children do not fit: go deeper first
+    nd += (int)__shfl(inc, nacc - 1, 64);
+    cur += nacc;
+  }
+  wave_sync();
+  return nd;
+}
+
+// All cliques of one root, lexicographic, by a depth-first walk over chunks of level-
+// synchronous prefix buffers (each level <= ECAP prefixes).  COUNT: returns the number of
+// cliques and ORs the clique-vertex lanes into *used.  FILL: writes the members of clique
+// out0 + t (t = 0, 1, ...) to A.members.
+template <int K, bool FILL>
+__device__ uint32_t root_cliques(const CliqueArgs& A, const RootInfo& R, int lane, WaveLds<K>& L,
+                                 uint64_t* used, int64_t out0) {
+  const uint64_t plast = L.pm[K - 1];
+  int n[K], cur[K];   // wave-uniform; constant-indexed through the unrolled switches below
+  uint32_t total = 0;
+  uint64_t usedl = 0;
+  if (lane == 0) {
+    Ent r0;
+    r0.M = ~0ull;
+    r0.P = 0;
+    L.buf[0][0] = r0;
+  }
+  wave_sync();
+#pragma unroll
+  for (int q = 0; q < K; ++q) { n[q] = 0; cur[q] = 0; }
+  n[0] = 1;
+  int D = 0;
+  for (;;) {
+    if (D == K - 2) {
+      // leaf level: the cliques of each prefix are its candidates in the last picker
+      int nl = 0;
+#pragma unroll
+      for (int q = 0; q < K - 1; ++q) if (q == D) nl = n[q];
+      const Ent* src = L.buf[K - 2];
+      if constexpr (!FILL) {
+        for (int e = lane; e < nl; e += 64) {
+          const Ent x = src[e];
+          const uint64_t c = x.M & plast;
+          total += (uint32_t)__popcll(c);
+          if (c) {
+            usedl |= c;
+#pragma unroll
+            for (int q = 0; q < K - 2; ++q) usedl |= 1ull << ((x.P >> (6 * q)) & 63);
+          }
+        }
+      } else {
+        // one prefix per lane (nl <= ECAP = 64), then the leaves spread over the lanes
+        uint64_t c = 0;
+        if (lane < nl) c = src[lane].M & plast;
+        const uint32_t cnt = (uint32_t)__popcll(c);
+        const uint32_t inc = wave_incl_scan(cnt, lane);
+        L.sc[lane] = inc;
+        const uint32_t T = __shfl(inc, 63, 64);
+        wave_sync();
+        for (uint32_t t = lane; t < T; t += 64) {
+          int lo = 0, hi = 63;   // first prefix with inclusive count > t
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (L.sc[mid] > t) hi = mid; else lo = mid + 1;
+          }
+          const Ent x = src[lo];
+          uint64_t cc = x.M & plast;
+          for (uint32_t r = t - (L.sc[lo] - (uint32_t)__popcll(cc)); r > 0; --r) cc &= cc - 1;
+          const int v = __builtin_ctzll(cc);
+          const int64_t j = out0 + total + t;
+          A.members[j * K] = R.r;
+#pragma unroll
+          for (int q = 0; q < K - 2; ++q)
+            A.members[j * K + 1 + q] = L.nb[(x.P >> (6 * q)) & 63];
+          A.members[j * K + K - 1] = L.nb[v];
+        }
+        total += T;
+        wave_sync();
+      }
+      if (D == 0) break;
+      --D;
+      continue;
+    }
+    int nD = 0, cD = 0;
+#pragma unroll
+    for (int q = 0; q < K - 1; ++q)
+      if (q == D) { nD = n[q]; cD = cur[q]; }
+    if (cD < nD) {
+      const int nd = expand<K>(L, D, cD, nD, lane);
+#pragma unroll
+      for (int q = 0; q < K - 1; ++q) {
+        if (q == D) cur[q] = cD;
+        if (q == D + 1) { n[q] = nd; cur[q] = 0; }
+      }
+      ++D;
+    } else {
+      if (D == 0) break;
+      --D;
+    }
+  }
+  if constexpr (!FILL) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) total += __shfl_xor(total, o, 64);
+    *used = wave_or(usedl);
+  }
+  return total;
+}
+
 template <int K>
 __global__ __launch_bounds__(CWG) void k5b_count(CliqueArgs A) {
-  __shared__ int32_t s_nb[CNW][RB_W];
-  __shared__ uint64_t s_adj[CNW][RB_W];
+  __shared__ WaveLds<K> s_w[CNW];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int w = blockIdx.x * CNW + wv;
   if (w >= A.n_roots) return;
   const RootInfo R = root_info(A, w);
   if (!R.ok) return;   // wave-uniform; counts were zeroed
-  int32_t* nb = s_nb[wv];
-  uint64_t* adj = s_adj[wv];
-  uint64_t pm[K];
-  neighbourhood<K>(A, R, lane, nb, adj, pm);
+  WaveLds<K>& L = s_w[wv];
+  neighbourhood<K>(A, R, lane, L);
   uint64_t used = 0;
-  uint32_t cnt = lane_count<K>(adj, pm, lane, used);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
-  used = wave_or(used);
+  uint32_t cnt;
+  if constexpr (K == 2) {
+    used = L.pm[1];
+    cnt = (uint32_t)__popcll(used);
+  } else {
+    cnt = root_cliques<K, false>(A, R, lane, L, &used, 0);
+  }
   if (lane == 0) {
     A.ccount[R.r] = (int32_t)cnt;
     if (cnt) A.in_clique[R.r] = 1;
   }
-  if (lane < R.d && ((used >> lane) & 1)) A.in_clique[nb[lane]] = 1;
+  if (lane < R.d && ((used >> lane) & 1)) A.in_clique[L.nb[lane]] = 1;
 }
 
 template <int K>
 __global__ __launch_bounds__(CWG) void k5b_fill(CliqueArgs A) {
-  __shared__ int32_t s_nb[CNW][RB_W];
-  __shared__ uint64_t s_adj[CNW][RB_W];
+  __shared__ WaveLds<K> s_w[CNW];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int w = blockIdx.x * CNW + wv;
   if (w >= A.n_roots) return;
   const RootInfo R = root_info(A, w);
   if (!R.ok) return;
-  int32_t* nb = s_nb[wv];
-  uint64_t* adj = s_adj[wv];
-  uint64_t pm[K];
-  neighbourhood<K>(A, R, lane, nb, adj, pm);
-  uint64_t used = 0;
-  const uint32_t n = lane_count<K>(adj, pm, lane, used);
-  // exclusive prefix of the lane counts (lane order = picker-1 member order)
-  uint32_t inc = n;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t t = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += t;
-  }
-  if (!n) return;
-  int64_t j = A.clique_off[R.r] + (inc - n);
-  int mem[K];
-  mem[0] = R.r;
-  mem[1] = nb[lane];
+  WaveLds<K>& L = s_w[wv];
+  neighbourhood<K>(A, R, lane, L);
+  const int64_t out0 = A.clique_off[R.r];
   if constexpr (K == 2) {
-    A.members[j * K] = mem[0];
-    A.members[j * K + 1] = mem[1];
+    const uint64_t c = L.pm[1];
+    if ((c >> lane) & 1) {
+      const int64_t j = out0 + __popcll(c & ((1ull << lane) - 1));
+      A.members[j * 2] = R.r;
+      A.members[j * 2 + 1] = L.nb[lane];
+    }
   } else {
-    BFill<K, 2>::run(adj, nb, pm, adj[lane], mem, A.members, j);
+    uint64_t used;
+    root_cliques<K, true>(A, R, lane, L, &used, out0);
   }
 }
 

@@ -7,7 +7,6 @@ namespace rgc {
 
 constexpr int MAX_K = 8;            // largest picker count with a compiled clique kernel
 constexpr int CELL_CAP = 8192;      // LDS counters per micrograph grid (k1_bin)
-constexpr int RANK_BUCKETS = 4096;  // LDS x-buckets for the row ranking (k7_rank)
 constexpr int SCAN_TILE = 2048;     // elements per scan workgroup
 
 // Uniform grid of one micrograph: cells of side `cell` (>= box_size) over its bounding box.
@@ -161,9 +160,10 @@ void launch_cc(hipStream_t stream, int phase, int N, int n_mg, int k, int get_cc
 // phase 0: count cliques per root + mark clique vertices; 1: write members; 2: ILP epilogue
 int launch_cliques(hipStream_t stream, int phase, int N, const CliqueArgs& A);
 int launch_cliques_dfs(hipStream_t stream, bool fill, int N, const CliqueArgs& A);
-void launch_rank(hipStream_t stream, int n_mg, int k, const int32_t* box_off, const double* x,
-                 const double* y, const uint8_t* in_clique, int32_t* vlist, int32_t* vsort,
-                 int32_t* vrow, MgStat* st);
+void launch_rank(hipStream_t stream, int N, int n_mg, int k, const int32_t* box_off,
+                 const int32_t* bmg, const MgGrid* grid, const double* x, const double* y,
+                 const uint8_t* in_clique, int32_t* bcnt, int32_t* bslot, int64_t* boff,
+                 int64_t* tile_buf, int64_t* total, int32_t* vsort, int32_t* vrow, MgStat* st);
 void launch_mg_offsets(hipStream_t stream, int n_mg, int k, const int32_t* box_off,
                        const int64_t* coff, int64_t* mg_off);
 

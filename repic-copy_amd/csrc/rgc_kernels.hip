@@ -10,8 +10,8 @@
 //   k5_cliques<K,..>  find_cliques (:49-56) for roots with more than RB_W forward
 //                     neighbours (the wavefront bitmap kernels of rgc_cliques.hip take the
 //                     rest; the ILP epilogue is k5_epilogue there)
-//   k7_rank           row index v.index() (:164,:193) as a per-micrograph rank by
-//                     (x, y, id)
+//   k7_*              row index v.index() (:164,:193) as a per-micrograph rank by
+//                     (x, y, id): x-bucket count -> scan -> scatter -> rank
 //
 // Floating point: every JI / degree / median operation keeps the reference's f64 operation
 // order; contraction into FMA is forbidden (the pragma below + -ffp-contract=off).
@@ -502,80 +502,70 @@ __global__ __launch_bounds__(WG) void k5_cliques(int N, CliqueArgs A) {
 
 // ----------------------------------------------------------------------------- K7 rows
 // Row index of each clique vertex = its rank by (x, y, id) among the micrograph's clique
-// vertices (v = sorted(set(...)); v.index(val), get_cliques.py:164,193).  Bucket the
-// vertices by x (monotone bucket map), then rank inside each bucket by counting.
-__global__ __launch_bounds__(WG) void k7_rank(int k, const int32_t* __restrict__ box_off,
-                                              const double* __restrict__ x,
-                                              const double* __restrict__ y,
-                                              const uint8_t* __restrict__ in_clique,
-                                              int32_t* vlist, int32_t* vsort, int32_t* vrow,
-                                              MgStat* st) {
-  __shared__ int32_t bcnt[RANK_BUCKETS];
-  __shared__ double redd[NW];
-  __shared__ int32_t nv;
-  const int m = blockIdx.x;
-  const int b0 = box_off[m * k], b1 = box_off[m * k + k];
-  if (threadIdx.x == 0) nv = 0;
-  __syncthreads();
-  double mn = INFINITY, mx = -INFINITY;
-  for (int g = b0 + threadIdx.x; g < b1; g += WG) {
-    if (in_clique[g]) {
-      const int pos = atomicAdd(&nv, 1);
-      vlist[b0 + pos] = g;
-      mn = fmin(mn, x[g]);
-      mx = fmax(mx, x[g]);
-    }
+// vertices (v = sorted(set(...)); v.index(val), get_cliques.py:164,193).  Thread-per-box
+// kernels over the whole sub-batch (a micrograph of 27k boxes is not serialised on one
+// workgroup): each micrograph owns n_m x-buckets (a monotone map of x over its bounding
+// box, at box-index offsets, so the buckets of all micrographs form one array); count ->
+// scan -> scatter; the rank is the bucket's start inside the micrograph plus the number of
+// smaller vertices in the bucket.
+__device__ __forceinline__ int rank_bucket(const MgGrid& G, int b0, int n, double x) {
+  const double ext = (double)G.gx * G.cell;
+  const double sc = ext > 0.0 && ext < INFINITY ? (double)n / ext : 0.0;
+  const double f = (x - G.minx) * sc;
+  return b0 + (int)fmin(fmax(f, 0.0), (double)(n - 1));
+}
+
+__global__ __launch_bounds__(WG) void k7_bucket(int N, int k, const int32_t* __restrict__ box_off,
+                                                const int32_t* __restrict__ bmg,
+                                                const MgGrid* __restrict__ grid,
+                                                const double* __restrict__ x,
+                                                const uint8_t* __restrict__ in_clique,
+                                                int32_t* bcnt, int32_t* bslot) {
+  const int g = blockIdx.x * WG + threadIdx.x;
+  if (g >= N || !in_clique[g]) return;
+  const int m = bmg[g];
+  const int b0 = box_off[m * k];
+  const int bk = rank_bucket(grid[m], b0, box_off[m * k + k] - b0, x[g]);
+  bslot[g] = atomicAdd(&bcnt[bk], 1);
+}
+
+template <bool RANK>
+__global__ __launch_bounds__(WG) void k7_place(int N, int k, const int32_t* __restrict__ box_off,
+                                               const int32_t* __restrict__ bmg,
+                                               const MgGrid* __restrict__ grid,
+                                               const double* __restrict__ x,
+                                               const double* __restrict__ y,
+                                               const uint8_t* __restrict__ in_clique,
+                                               const int64_t* __restrict__ boff,
+                                               const int32_t* __restrict__ bslot, int32_t* vsort,
+                                               int32_t* vrow) {
+  const int g = blockIdx.x * WG + threadIdx.x;
+  if (g >= N || !in_clique[g]) return;
+  const int m = bmg[g];
+  const int b0 = box_off[m * k];
+  const double gx = x[g];
+  const int bk = rank_bucket(grid[m], b0, box_off[m * k + k] - b0, gx);
+  const int64_t lo = boff[bk];
+  if (!RANK) {
+    vsort[lo + bslot[g]] = g;
+    return;
   }
-  mn = block_min(mn, redd);
-  mx = block_max(mx, redd);
-  const int V = nv;
-  if (threadIdx.x == 0) st[m].n_vert = V;
-  if (V == 0) return;
-  const int nb = min(V, RANK_BUCKETS);
-  const double scale = mx > mn ? (double)nb / (mx - mn) : 0.0;
-  for (int b = threadIdx.x; b < nb; b += WG) bcnt[b] = 0;
-  __syncthreads();
-  for (int i = threadIdx.x; i < V; i += WG) {
-    const int g = vlist[b0 + i];
-    const int bk = min(nb - 1, (int)((x[g] - mn) * scale));
-    atomicAdd(&bcnt[bk], 1);
+  const int64_t hi = boff[bk + 1];
+  const double gy = y[g];
+  int r = (int)(lo - boff[b0]);
+  for (int64_t q = lo; q < hi; ++q) {
+    const int u = vsort[q];
+    const double ux = x[u], uy = y[u];
+    r += (ux < gx) || (ux == gx && (uy < gy || (uy == gy && u < g)));
   }
-  __syncthreads();
-  {  // exclusive scan of bcnt[0..nb)
-    __shared__ int64_t red64[NW];
-    const int per = (nb + WG - 1) / WG;
-    const int c0 = min((int)threadIdx.x * per, nb), c1 = min(c0 + per, nb);
-    int64_t s = 0;
-    for (int c = c0; c < c1; ++c) s += bcnt[c];
-    int64_t tot;
-    int64_t pre = block_excl_scan(s, red64, &tot);
-    for (int c = c0; c < c1; ++c) {
-      const int v = bcnt[c];
-      bcnt[c] = (int)pre;
-      pre += v;
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < V; i += WG) {
-    const int g = vlist[b0 + i];
-    const int bk = min(nb - 1, (int)((x[g] - mn) * scale));
-    vsort[b0 + atomicAdd(&bcnt[bk], 1)] = g;
-  }
-  __syncthreads();
-  // after the scatter bcnt[b] = end of bucket b = start of bucket b + 1
-  for (int i = threadIdx.x; i < V; i += WG) {
-    const int g = vlist[b0 + i];
-    const double gx = x[g], gy = y[g];
-    const int bk = min(nb - 1, (int)((gx - mn) * scale));
-    const int lo = bk > 0 ? bcnt[bk - 1] : 0, hi = bcnt[bk];
-    int r = lo;
-    for (int q = lo; q < hi; ++q) {
-      const int u = vsort[b0 + q];
-      const double ux = x[u], uy = y[u];
-      r += (ux < gx) || (ux == gx && (uy < gy || (uy == gy && u < g)));
-    }
-    vrow[g] = r;
-  }
+  vrow[g] = r;
+}
+
+__global__ __launch_bounds__(WG) void k7_nvert(int n_mg, int k, const int32_t* __restrict__ box_off,
+                                               const int64_t* __restrict__ boff, MgStat* st) {
+  const int m = blockIdx.x * WG + threadIdx.x;
+  if (m >= n_mg) return;
+  st[m].n_vert = (int)(boff[box_off[m * k + k]] - boff[box_off[m * k]]);
 }
 
 __global__ __launch_bounds__(WG) void k_mg_offsets(int n_mg, int k, const int32_t* __restrict__ box_off,
@@ -733,10 +723,20 @@ int launch_cliques_dfs(hipStream_t stream, bool fill, int N, const CliqueArgs& A
   return 0;
 }
 
-void launch_rank(hipStream_t stream, int n_mg, int k, const int32_t* box_off, const double* x,
-                 const double* y, const uint8_t* in_clique, int32_t* vlist, int32_t* vsort,
-                 int32_t* vrow, MgStat* st) {
-  RGC_LAUNCH(k7_rank, n_mg, WG, k, box_off, x, y, in_clique, vlist, vsort, vrow, st);
+void launch_rank(hipStream_t stream, int N, int n_mg, int k, const int32_t* box_off,
+                 const int32_t* bmg, const MgGrid* grid, const double* x, const double* y,
+                 const uint8_t* in_clique, int32_t* bcnt, int32_t* bslot, int64_t* boff,
+                 int64_t* tile_buf, int64_t* total, int32_t* vsort, int32_t* vrow, MgStat* st) {
+  const int nb = (N + WG - 1) / WG;
+  if (nb) RGC_LAUNCH(k7_bucket, nb, WG, N, k, box_off, bmg, grid, x, in_clique, bcnt, bslot);
+  launch_scan(stream, N, bcnt, boff, tile_buf, total);
+  if (nb) {
+    RGC_LAUNCH(k7_place<false>, nb, WG, N, k, box_off, bmg, grid, x, y, in_clique, boff, bslot,
+               vsort, vrow);
+    RGC_LAUNCH(k7_place<true>, nb, WG, N, k, box_off, bmg, grid, x, y, in_clique, boff, bslot,
+               vsort, vrow);
+  }
+  RGC_LAUNCH(k7_nvert, (n_mg + WG - 1) / WG, WG, n_mg, k, box_off, boff, st);
 }
 
 void launch_mg_offsets(hipStream_t stream, int n_mg, int k, const int32_t* box_off,
