@@ -58,7 +58,8 @@ enum DevBufId {
   D_SUBMG, D_SUBX, D_SUBY, D_SUBS, D_ORIG, D_STAMPS,
   D_BOXOFF, D_CELLOFF, D_P0OFF, D_IDBASE, D_GRID, D_CELLSTART, D_SX, D_SY, D_SBOX, D_SPICK, D_SMG, D_BMG,
   D_BPICK, D_FWDCNT, D_FWDOFF, D_TILES, D_TOTAL, D_EDST, D_EJI, D_PARENT, D_HASEDGE, D_CSIZE,
-  D_STAT, D_INSKEY, D_COMPMIN, D_CCOUNT, D_COFF, D_INCL, D_VLIST, D_VSORT, D_VROW, D_BOFF, D_MGOFF,
+  D_STAT, D_INSKEY, D_COMPMIN, D_CCOUNT, D_COFF, D_INCL, D_VLIST, D_VSORT, D_VROW, D_BOFF, D_RLO, D_ADJG, D_RBOUND, D_RFLAG, D_DFSMG,
+  D_LCNT, D_LOFF, D_LROOT0, D_LROOT1, D_LM0, D_LM1, D_LP0, D_LP1,
   // RGC_F_EDGES test hook
   D_EU, D_EV, D_EJIOUT,
   D_COUNT
@@ -284,7 +285,7 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   TRY(ensure_dev(c, D_FWDCNT, N * 4));
   TRY(ensure_dev(c, D_FWDOFF, (N + 1) * 8));
   TRY(ensure_dev(c, D_TILES, scan_tiles_needed(N + 1) * 8));
-  TRY(ensure_dev(c, D_TOTAL, 16));
+  TRY(ensure_dev(c, D_TOTAL, 32));
   TRY(ensure_dev(c, D_PARENT, N * 4));
   TRY(ensure_dev(c, D_HASEDGE, N));
   TRY(ensure_dev(c, D_CSIZE, N * 4));
@@ -298,10 +299,13 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   TRY(ensure_dev(c, D_VSORT, N * 4));
   TRY(ensure_dev(c, D_VROW, N * 4));
   TRY(ensure_dev(c, D_BOFF, (N + 1) * 8));
-  TRY(ensure_dev(c, D_MGOFF, (n_mg + 1) * 8));
-  TRY(ensure_host(c, H_TOTAL, 16));
+  TRY(ensure_dev(c, D_RLO, 2 * (size_t)n_mg * 8 + 8));
+  TRY(ensure_host(c, H_TOTAL, 32));
   TRY(ensure_host(c, H_STAT, n_mg * sizeof(MgStat)));
-  TRY(ensure_host(c, H_MGOFF, (n_mg + 1) * 8));
+  TRY(ensure_host(c, H_MGOFF, 2 * (size_t)n_mg * 8 + 8));
+  TRY(ensure_dev(c, D_RBOUND, N * 8));
+  TRY(ensure_dev(c, D_RFLAG, N));
+  TRY(ensure_dev(c, D_DFSMG, n_mg));
 
   hipStream_t s = c->stream;
   TRY(mark(c, "h2d_meta"));
@@ -315,6 +319,8 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   HIPCHK(hipMemsetAsync(D<void>(c, D_INCL), 0, N, s));
   HIPCHK(hipMemsetAsync(D<void>(c, D_CCOUNT), 0, N * 4, s));
   HIPCHK(hipMemsetAsync(D<void>(c, D_VLIST), 0, N * 4, s));   // row-rank bucket counters
+  HIPCHK(hipMemsetAsync(D<void>(c, D_RFLAG), 0, N, s));
+  HIPCHK(hipMemsetAsync(D<void>(c, D_DFSMG), 0, n_mg, s));
   HIPCHK(hipMemsetAsync(D<void>(c, D_INSKEY), 0xff, N * 8, s));
   if (get_cc) HIPCHK(hipMemsetAsync(D<void>(c, D_COMPMIN), 0xff, N * 8, s));
 
@@ -339,6 +345,7 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   const int64_t E = H<int64_t>(c, H_TOTAL)[0];
   *E_out = E;
   TRY(ensure_dev(c, D_EDST, E * 4));
+  TRY(ensure_dev(c, D_ADJG, E * 8));
   TRY(ensure_dev(c, D_EJI, E * 8));
   TRY(mark(c, "k2_pairs_fill"));
   launch_pairs(s, true, (int)N, k, B, two_b2, bo, D<int32_t>(c, D_CELLOFF), D<MgGrid>(c, D_GRID),
@@ -368,53 +375,97 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   A.ins_key = D<unsigned long long>(c, D_INSKEY); A.clique_off = D<int64_t>(c, D_COFF);
   A.vrow = D<int32_t>(c, D_VROW);
   A.ccount = D<int32_t>(c, D_CCOUNT); A.in_clique = D<uint8_t>(c, D_INCL);
+  A.adjg = D<uint64_t>(c, D_ADJG); A.rbound = D<uint64_t>(c, D_RBOUND);
+  A.rflag = D<uint8_t>(c, D_RFLAG); A.dfs_mg = D<uint8_t>(c, D_DFSMG); A.dfs_base = 0;
   A.members = nullptr; A.rows = nullptr; A.w = nullptr; A.conf = nullptr; A.consensus = nullptr;
   A.order = nullptr;
-  TRY(mark(c, "k5_cliques_count"));
-  if (launch_cliques(s, 0, (int)N, A) != 0) return fail("unsupported k");
-  TRY(mark(c, "scan_cliques"));
+  int64_t* d_tot = D<int64_t>(c, D_TOTAL);   // [0] edges, [1] DFS cliques, [2] level, [3] rank
+  int64_t* h_tot = H<int64_t>(c, H_TOTAL);
+  TRY(mark(c, "k5_setup"));   // DFS routing, neighbourhood bitmaps
+  launch_clique_setup(s, (int)N, A);
+  TRY(mark(c, "k5_dfs_count"));   // (micrographs with a root of > RB_W neighbours only)
+  if (launch_cliques_dfs(s, false, (int)N, A) != 0) return fail("unsupported k");
   launch_scan(s, N, D<int32_t>(c, D_CCOUNT), D<int64_t>(c, D_COFF), D<int64_t>(c, D_TILES),
-              D<int64_t>(c, D_TOTAL));
-  HIPCHK(hipMemcpyAsync(H<int64_t>(c, H_TOTAL), D<int64_t>(c, D_TOTAL), 8,
-                        hipMemcpyDeviceToHost, s));
-  // row ranks need only the clique-vertex flags of the count pass: queued before the host
-  // waits for the clique total (bucket counters in D_VLIST, slots in D_CSIZE: the CC sizes
-  // are dead by now; the scan total goes to the second D_TOTAL slot)
+              d_tot + 1);
+  // prefix levels: count -> scan -> (host reads the size) -> fill, ping-pong item buffers
+  LevelArgs L;
+  L.D = 0; L.n_items = N; L.in_root = nullptr; L.in_M = nullptr; L.in_P = nullptr;
+  L.cnt = nullptr; L.off = nullptr; L.out_root = nullptr; L.out_M = nullptr; L.out_P = nullptr;
+  int cur = 0;
+  int64_t C1 = 0, C2 = 0;
+  for (int lv = 0; lv <= k - 2; ++lv) {
+    const bool first = lv == 0, leaf = lv == k - 2;
+    L.D = lv;
+    TRY(ensure_dev(c, D_LCNT, L.n_items * 4));
+    TRY(ensure_dev(c, D_LOFF, (L.n_items + 1) * 8));
+    TRY(ensure_dev(c, D_TILES, scan_tiles_needed(L.n_items + 1) * 8));
+    L.cnt = D<int32_t>(c, D_LCNT);
+    L.off = D<int64_t>(c, D_LOFF);
+    TRY(mark(c, leaf ? "k5_leaf_count" : "k5_level_count"));
+    if (first) HIPCHK(hipMemsetAsync(L.cnt, 0, N * 4, s));   // non-roots stay 0
+    if (launch_clique_level(s, first, leaf, false, A, L) != 0) return fail("unsupported k");
+    launch_scan(s, L.n_items, L.cnt, D<int64_t>(c, D_LOFF), D<int64_t>(c, D_TILES), d_tot + 2);
+    HIPCHK(hipMemcpyAsync(h_tot + 1, d_tot + 1, 16, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+    const int64_t nn = h_tot[2];
+    C2 = h_tot[1];
+    if (leaf) {
+      C1 = nn;
+      break;
+    }
+    const int o = cur ^ 1;
+    TRY(ensure_dev(c, D_LROOT0 + o, nn * 4));
+    TRY(ensure_dev(c, D_LM0 + o, nn * 8));
+    TRY(ensure_dev(c, D_LP0 + o, nn * 8));
+    L.out_root = D<int32_t>(c, D_LROOT0 + o);
+    L.out_M = D<uint64_t>(c, D_LM0 + o);
+    L.out_P = D<uint64_t>(c, D_LP0 + o);
+    TRY(mark(c, "k5_level_fill"));
+    launch_clique_level(s, first, false, true, A, L);
+    L.in_root = L.out_root; L.in_M = L.out_M; L.in_P = L.out_P;
+    L.n_items = nn;
+    cur = o;
+  }
+  // row ranks need only the clique-vertex flags of the count passes (bucket counters in
+  // D_VLIST, slots in D_CSIZE: the CC sizes are dead by now)
   TRY(mark(c, "k7_rank"));
   launch_rank(s, (int)N, n_mg, k, bo, D<int32_t>(c, D_BMG), D<MgGrid>(c, D_GRID), x, y,
               D<uint8_t>(c, D_INCL), D<int32_t>(c, D_VLIST), D<int32_t>(c, D_CSIZE),
-              D<int64_t>(c, D_BOFF), D<int64_t>(c, D_TILES), D<int64_t>(c, D_TOTAL) + 1,
+              D<int64_t>(c, D_BOFF), D<int64_t>(c, D_TILES), d_tot + 3,
               D<int32_t>(c, D_VSORT), D<int32_t>(c, D_VROW), D<MgStat>(c, D_STAT));
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(s));
-  const int64_t C = H<int64_t>(c, H_TOTAL)[0];
+  const int64_t C = C1 + C2;
   *C_out = C;
   TRY(ensure_outputs(c, out_base + C, out_base, k, true, multi != 0));
   A.C = C;
+  A.dfs_base = C1;
   A.members = D<int32_t>(c, D_MEMBERS) + out_base * k;
   A.rows = D<int32_t>(c, D_ROWS) + out_base * k;
   A.w = D<float>(c, D_W) + out_base;
   A.conf = D<float>(c, D_CONF) + out_base;
   A.consensus = D<int32_t>(c, D_CONS) + out_base;
   A.order = multi ? D<uint8_t>(c, D_ORDER) + out_base * k : nullptr;
-  TRY(mark(c, "k5_cliques_fill"));
-  launch_cliques(s, 1, (int)N, A);
+  TRY(mark(c, "k5_leaf_fill"));
+  launch_clique_level(s, k == 2, true, true, A, L);
+  TRY(mark(c, "k5_dfs_fill"));
+  launch_cliques_dfs(s, true, (int)N, A);
   TRY(mark(c, "k5_epilogue"));
-  launch_cliques(s, 2, (int)N, A);
-  TRY(mark(c, "k_mg_offsets"));
-  launch_mg_offsets(s, n_mg, k, bo, D<int64_t>(c, D_COFF), D<int64_t>(c, D_MGOFF));
+  launch_clique_epilogue(s, A);
+  TRY(mark(c, "k5_ranges"));
+  launch_clique_ranges(s, A, C1, D<int64_t>(c, D_RLO), D<int64_t>(c, D_RLO) + n_mg);
   HIPCHK(hipMemcpyAsync(H<void>(c, H_STAT), D<void>(c, D_STAT), n_mg * sizeof(MgStat),
                         hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOFF), D<void>(c, D_MGOFF), (n_mg + 1) * 8,
+  HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOFF), D<void>(c, D_RLO), 2 * (size_t)n_mg * 8,
                         hipMemcpyDeviceToHost, s));
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
   const MgStat* st = H<MgStat>(c, H_STAT);
-  const int64_t* mo = H<int64_t>(c, H_MGOFF);
+  const int64_t* rlo = H<int64_t>(c, H_MGOFF);
+  const int64_t* rhi = rlo + n_mg;
   st_out.assign(st, st + n_mg);
   for (int m = 0; m < n_mg; ++m) {
-    st_out[m].clique_base = out_base + mo[m];
-    st_out[m].clique_cnt = mo[m + 1] - mo[m];
+    st_out[m].clique_base = out_base + rlo[m];
+    st_out[m].clique_cnt = rhi[m] - rlo[m];
     if (st_out[m].status == RGC_OK && st_out[m].clique_cnt == 0) st_out[m].status = RGC_NO_CLIQUES;
   }
   return 0;

@@ -6,330 +6,233 @@
 // one-box-per-picker k-tuples that are pairwise adjacent.  Every such tuple has one picker-0
 // member, its "root"; the other k-1 members are forward neighbours of the root.
 //
-// One WAVEFRONT per root:
-//   * lane i holds the i-th forward neighbour of the root (sorted by box index, so the
-//     neighbours of picker p form one contiguous run of lanes);
-//   * each lane merges its own forward list against the neighbourhood and keeps the result
-//     as a 64-bit adjacency row in LDS; one ballot per picker gives the picker masks;
-//   * the cliques of the root are then the picker-by-picker choices v1 in pm[1],
-//     v2 in pm[2] & adj[v1], v3 in pm[3] & adj[v1] & adj[v2], ... : bitwise ANDs and ctz,
-//     no list intersections; lane v1 walks the subtree of its own picker-1 choice and the
-//     last level is a popcount.
-// COUNT writes the clique count of every root and flags the clique vertices (for the row
-// ranks); FILL recomputes the per-lane counts, scans them across the wave and writes the
-// members at the root's scanned offset: lexicographic order, deterministic.  The ILP
-// epilogue runs one THREAD per clique afterwards (balanced, coalesced output stores).
-// Roots with more than RB_W forward neighbours go to the thread-per-root DFS in
-// rgc_kernels.hip, which writes into the same arrays.
+// 1. Neighbourhood bitmaps (k5n_build): a group of G lanes per root (G = 16: four roots per
+//    wavefront; G = 64 for roots with 17..64 forward neighbours).  Lane i holds the i-th
+//    forward neighbour (sorted by box index, so each picker is a contiguous run of lanes);
+//    its adjacency row inside the neighbourhood (a 64-bit mask, forward edges only) goes to
+//    adjg[fwd_off[root] + i] and the picker run starts to rbound[root].
+// 2. Level-synchronous prefix expansion over the whole sub-batch (k5l<K, ...>): a level-D
+//    prefix = (root, mask M of neighbourhood lanes adjacent to all chosen members, chosen
+//    lanes P, 6 bits each); its children are the picker-(D+1) lanes v in M, with mask
+//    M & adj[v].  One THREAD per prefix, count -> scan -> fill per level, so the work of a
+//    root with 27k cliques (C5) is spread over the GPU instead of serialised on one lane or
+//    wave.  A child is kept only when it can still be completed (it has a candidate in
+//    picker D+2).  At the last level the cliques of a prefix are its candidate lanes in the
+//    last picker: COUNT flags the clique vertices (row ranks), FILL writes members.  Items
+//    stay in parent order, so cliques come out lexicographic (deterministic) and grouped by
+//    root, hence by micrograph.
+// 3. The ILP epilogue: one THREAD per clique (balanced, coalesced output stores).
+// Micrographs with a root of more than RB_W forward neighbours run through the
+// thread-per-root DFS of rgc_kernels.hip instead (their cliques follow the others).
 #pragma clang fp contract(off)
 
 #include "rgc_device.h"
 #include "rgc_kernels.h"
 
+#include <climits>
+
 namespace rgc {
 
-constexpr int CWG = 256;            // 4 wavefronts (roots) per workgroup
-constexpr int CNW = CWG / 64;
+__device__ __forceinline__ uint64_t mask_below(int n) { return n >= 64 ? ~0ull : ((1ull << n) - 1); }
 
-__device__ __forceinline__ void wave_sync() {
-  // LDS written by other lanes of this wavefront becomes visible (and is not reordered)
+// lanes of picker p (1..K-1) in a root's neighbourhood: byte p-1 of rbound = first lane of
+// picker p, byte p = first lane after it (byte K-1 = d)
+__device__ __forceinline__ uint64_t picker_lanes(uint64_t rb, int p) {
+  const int s = (int)((rb >> (8 * (p - 1))) & 0xFF);
+  const int e = (int)((rb >> (8 * p)) & 0xFF);
+  return mask_below(e) & ~mask_below(s);
+}
+
+// valid clique root: picker-0 box with forward edges in a finished micrograph (and in the
+// --get_cc target component)
+__device__ __forceinline__ bool root_valid(const CliqueArgs& A, int g, int m) {
+  if (A.bpick[g] != 0 || A.fwd_off[g] == A.fwd_off[g + 1]) return false;
+  const MgStat s = A.st[m];
+  return s.status == 0 && (!(A.flags & 1) || A.parent[g] == s.target);
+}
+
+// micrographs with a root of more than RB_W forward neighbours take the DFS route
+__global__ __launch_bounds__(WG) void k5_route(int N, CliqueArgs A) {
+  const int g = blockIdx.x * WG + threadIdx.x;
+  if (g >= N) return;
+  const int m = A.bmg[g];
+  if (root_valid(A, g, m) && A.fwd_off[g + 1] - A.fwd_off[g] > RB_W) A.dfs_mg[m] = 1;
+}
+
+template <int G>
+__global__ __launch_bounds__(WG) void k5n_build(int, CliqueArgs A) {
+  constexpr int NG = WG / G;
+  __shared__ int32_t s_nb[NG][G];
+  const int grp = threadIdx.x / G, lane = threadIdx.x % G;
+  const int w = blockIdx.x * NG + grp;   // one group per picker-0 box
+  if (w >= A.n_roots) return;
+  int m = 0;
+  {
+    int hi = A.n_mg;
+    while (hi - m > 1) {
+      const int mid = (m + hi) >> 1;
+      if (A.p0off[mid] <= w) m = mid; else hi = mid;
+    }
+  }
+  const int g = A.box_off[m * A.k] + (w - A.p0off[m]);
+  if (!root_valid(A, g, m) || A.dfs_mg[m]) return;
+  const int64_t lo = A.fwd_off[g];
+  const int d = (int)(A.fwd_off[g + 1] - lo);
+  if (d > G || (G > 16 && d <= 16)) return;   // the other launch's root
+  int32_t* nb = s_nb[grp];
+  int u = -1, pk = A.k;
+  if (lane < d) {
+    u = A.e_dst[lo + lane];
+    pk = A.bpick[u];
+    nb[lane] = u;
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-struct RootInfo {
-  int r;        // root box (sub-batch index)
-  int d;        // forward neighbours
-  int64_t lo;   // start of its forward list
-  bool ok;      // enumerated by the wavefront kernels
-};
-
-// wavefront w -> the w-th picker-0 box of the sub-batch (micrograph by binary search)
-__device__ __forceinline__ RootInfo root_info(const CliqueArgs& A, int w) {
-  int lo = 0, hi = A.n_mg;
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (A.p0off[mid] <= w) lo = mid; else hi = mid;
-  }
-  const int m = lo;
-  RootInfo R;
-  R.r = A.box_off[m * A.k] + (w - A.p0off[m]);
-  R.lo = A.fwd_off[R.r];
-  const int64_t d = A.fwd_off[R.r + 1] - R.lo;
-  R.d = (int)d;
-  const MgStat s = A.st[m];
-  R.ok = d > 0 && d <= RB_W && s.status == 0 && (!(A.flags & 1) || A.parent[R.r] == s.target);
-  return R;
-}
-
-constexpr int ECAP = 64;            // prefixes per level buffer (per wavefront)
-
-// A prefix of a root's clique: members for pickers 1..D as neighbourhood lanes (6 bits each,
-// picker q at bits 6(q-1)) and the mask of neighbourhood lanes adjacent to all of them.
-struct Ent {
-  uint64_t M;
-  uint64_t P;
-};
-
-// per-wavefront LDS
-template <int K>
-struct WaveLds {
-  int32_t nb[RB_W];           // neighbourhood (forward neighbours of the root), sorted
-  uint64_t adj[RB_W];         // adj[i]: neighbourhood lanes adjacent to lane i (forward)
-  uint64_t pm[K];             // pm[p]: neighbourhood lanes of picker p
-  Ent buf[K - 1][ECAP];       // level D prefixes (D = 0..K-2; level 0 = the root alone)
-  uint32_t sc[ECAP];          // fill: inclusive scan of the leaf counts of the leaf level
-};
-
-// neighbourhood of the root: nb, adj, pm
-template <int K>
-__device__ __forceinline__ void neighbourhood(const CliqueArgs& A, const RootInfo& R, int lane,
-                                              WaveLds<K>& L) {
-  int u = -1, pk = -1;
-  if (lane < R.d) {
-    u = A.e_dst[R.lo + lane];
-    pk = A.bpick[u];
-    L.nb[lane] = u;
-  }
-  wave_sync();
-  uint64_t mask = 0;
-  if (lane < R.d) {
-    // merge u's sorted forward list with the sorted neighbourhood (targets of u sort after u)
-    int64_t e = A.fwd_off[u];
-    const int64_t e1 = A.fwd_off[u + 1];
-    int j = lane + 1;
-    int v = j < R.d ? L.nb[j] : 0;
-    while (e < e1 && j < R.d) {
-      const int t = A.e_dst[e];
-      if (t < v) {
-        ++e;
-      } else {
-        if (t == v) { mask |= 1ull << j; ++e; }
-        ++j;
-        v = j < R.d ? L.nb[j] : 0;
-      }
-    }
-  }
-  L.adj[lane] = mask;
+  if (lane < d) {
+    // adjacency row: u's forward targets looked up in the sorted neighbourhood (only lanes
+    // after u can match); four loads in flight per step
+    uint64_t mask = 0;
+    const int64_t e0 = A.fwd_off[u], e1 = A.fwd_off[u + 1];
+    const int last = nb[d - 1];
+    for (int64_t e = e0; e < e1; e += 4) {
+      int t[4];
 #pragma unroll
-  for (int p = 0; p < K; ++p) {
-    const uint64_t b = __ballot(pk == p);
-    if (lane == 0) L.pm[p] = b;
-  }
-  wave_sync();
-}
-
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+      for (int q = 0; q < 4; ++q) t[q] = e + q < e1 ? A.e_dst[e + q] : INT_MAX;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t t = __shfl_up(v, o, 64);
-    if (lane >= o) v += t;
-  }
-  return v;
-}
-
-__device__ __forceinline__ uint64_t wave_or(uint64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
-  return v;
-}
-
-// Expand level-D prefixes, from *cur on, into the (empty) level D+1 buffer until it is full.
-// A child is kept only if it can still be completed (it has a candidate in picker D+2).
-// Wave-cooperative: one prefix per lane, children placed by a wave scan; whole prefixes
-// only, in order, so level D+1 stays lexicographic.  Returns the children written.
-template <int K>
-__device__ int expand(WaveLds<K>& L, int D, int& cur, int n_src, int lane) {
-  const uint64_t pnext = L.pm[D + 1];
-  const uint64_t pafter = D + 2 < K ? L.pm[D + 2] : ~0ull;
-  Ent* src = L.buf[D];
-  Ent* dst = L.buf[D + 1];
-  int nd = 0;
-  while (cur < n_src && nd < ECAP) {
-    const int e = cur + lane;
-    Ent x = {0, 0};
-    uint32_t cnt = 0;
-    if (e < n_src) {
-      x = src[e];
-      uint64_t c = x.M & pnext;
-      while (c) {
-        const int v = __builtin_ctzll(c);
-        c &= c - 1;
-        cnt += (x.M & L.adj[v] & pafter) ? 1u : 0u;
-      }
-    }
-    const uint32_t inc = wave_incl_scan(cnt, lane);
-    const bool ok = e < n_src && (int)inc <= ECAP - nd;
-    const int nacc = __popcll(__ballot(ok));
-    if (ok && cnt) {
-      int o = nd + (int)(inc - cnt);
-      uint64_t c = x.M & pnext;
-      while (c) {
-        const int v = __builtin_ctzll(c);
-        c &= c - 1;
-        const uint64_t m2 = x.M & L.adj[v];
-        if (m2 & pafter) {
-          Ent y;
-          y.M = m2;
-          y.P = x.P | ((uint64_t)v << (6 * D));
-          dst[o++] = y;
+      for (int q = 0; q < 4; ++q) {
+        if (t[q] > last) continue;
+        int a = lane + 1, b = d;   // first lane with nb >= t
+        while (a < b) {
+          const int mid = (a + b) >> 1;
+          if (nb[mid] < t[q]) a = mid + 1; else b = mid;
         }
+        if (a < d && nb[a] == t[q]) mask |= 1ull << a;
       }
+      if (t[3] >= last) break;
     }
-    if (nacc == 0) break;   // the next prefix's children do not fit: go deeper first
-    nd += (int)__shfl(inc, nacc - 1, 64);
-    cur += nacc;
+    A.adjg[lo + lane] = mask;
   }
-  wave_sync();
-  return nd;
-}
-
-// All cliques of one root, lexicographic, by a depth-first walk over chunks of level-
-// synchronous prefix buffers (each level <= ECAP prefixes).  COUNT: returns the number of
-// cliques and ORs the clique-vertex lanes into *used.  FILL: writes the members of clique
-// out0 + t (t = 0, 1, ...) to A.members.
-template <int K, bool FILL>
-__device__ uint32_t root_cliques(const CliqueArgs& A, const RootInfo& R, int lane, WaveLds<K>& L,
-                                 uint64_t* used, int64_t out0) {
-  const uint64_t plast = L.pm[K - 1];
-  int n[K], cur[K];   // wave-uniform; constant-indexed through the unrolled switches below
-  uint32_t total = 0;
-  uint64_t usedl = 0;
+  // picker runs: lanes are sorted picker-major, so the first lane of picker p = #lanes below p
+  const uint64_t gmask = (G == 64 ? ~0ull : (((1ull << G) - 1) << ((threadIdx.x & 63) / G * G)));
+  uint64_t rb = 0;
+#pragma unroll
+  for (int p = 1; p < MAX_K; ++p) {
+    const uint64_t below = __ballot(lane < d && pk < p) & gmask;
+    const int s = __popcll(below);
+    if (p < A.k) rb |= (uint64_t)s << (8 * (p - 1));
+  }
+  rb |= (uint64_t)d << (8 * (A.k - 1));
   if (lane == 0) {
-    Ent r0;
-    r0.M = ~0ull;
-    r0.P = 0;
-    L.buf[0][0] = r0;
+    A.rbound[g] = rb;
+    A.rflag[g] = 1;
   }
-  wave_sync();
+}
+
+// One level of prefix expansion (thread per prefix).  FIRST: the prefixes are the roots
+// themselves (thread per box, M = all lanes).  LEAF: the children are cliques.
+template <int K, bool FIRST, bool LEAF, bool FILL>
+__global__ __launch_bounds__(WG) void k5l(CliqueArgs A, LevelArgs L) {
+  const int64_t i = (int64_t)blockIdx.x * WG + threadIdx.x;
+  if (i >= L.n_items) return;
+  int r;
+  uint64_t M, P;
+  if (FIRST) {
+    r = (int)i;
+    if (!A.rflag[r]) return;   // cnt stays 0 (zeroed)
+    M = ~0ull;
+    P = 0;
+  } else {
+    r = L.in_root[i];
+    M = L.in_M[i];
+    P = L.in_P[i];
+  }
+  const int D = L.D;   // members chosen so far (pickers 1..D)
+  const uint64_t rb = A.rbound[r];
+  const int64_t lo = A.fwd_off[r];
+  uint64_t c = M & picker_lanes(rb, D + 1);
+  if (LEAF) {
+    if (!FILL) {
+      L.cnt[i] = __popcll(c);
+      if (c) {
+        A.in_clique[r] = 1;
 #pragma unroll
-  for (int q = 0; q < K; ++q) { n[q] = 0; cur[q] = 0; }
-  n[0] = 1;
-  int D = 0;
-  for (;;) {
-    if (D == K - 2) {
-      // leaf level: the cliques of each prefix are its candidates in the last picker
-      int nl = 0;
-#pragma unroll
-      for (int q = 0; q < K - 1; ++q) if (q == D) nl = n[q];
-      const Ent* src = L.buf[K - 2];
-      if constexpr (!FILL) {
-        for (int e = lane; e < nl; e += 64) {
-          const Ent x = src[e];
-          const uint64_t c = x.M & plast;
-          total += (uint32_t)__popcll(c);
-          if (c) {
-            usedl |= c;
-#pragma unroll
-            for (int q = 0; q < K - 2; ++q) usedl |= 1ull << ((x.P >> (6 * q)) & 63);
-          }
+        for (int q = 0; q < K - 2; ++q) A.in_clique[A.e_dst[lo + ((P >> (6 * q)) & 63)]] = 1;
+        while (c) {
+          const int v = __builtin_ctzll(c);
+          c &= c - 1;
+          A.in_clique[A.e_dst[lo + v]] = 1;
         }
-      } else {
-        // one prefix per lane (nl <= ECAP = 64), then the leaves spread over the lanes
-        uint64_t c = 0;
-        if (lane < nl) c = src[lane].M & plast;
-        const uint32_t cnt = (uint32_t)__popcll(c);
-        const uint32_t inc = wave_incl_scan(cnt, lane);
-        L.sc[lane] = inc;
-        const uint32_t T = __shfl(inc, 63, 64);
-        wave_sync();
-        for (uint32_t t = lane; t < T; t += 64) {
-          int lo = 0, hi = 63;   // first prefix with inclusive count > t
-          while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (L.sc[mid] > t) hi = mid; else lo = mid + 1;
-          }
-          const Ent x = src[lo];
-          uint64_t cc = x.M & plast;
-          for (uint32_t r = t - (L.sc[lo] - (uint32_t)__popcll(cc)); r > 0; --r) cc &= cc - 1;
-          const int v = __builtin_ctzll(cc);
-          const int64_t j = out0 + total + t;
-          A.members[j * K] = R.r;
-#pragma unroll
-          for (int q = 0; q < K - 2; ++q)
-            A.members[j * K + 1 + q] = L.nb[(x.P >> (6 * q)) & 63];
-          A.members[j * K + K - 1] = L.nb[v];
-        }
-        total += T;
-        wave_sync();
       }
-      if (D == 0) break;
-      --D;
-      continue;
-    }
-    int nD = 0, cD = 0;
-#pragma unroll
-    for (int q = 0; q < K - 1; ++q)
-      if (q == D) { nD = n[q]; cD = cur[q]; }
-    if (cD < nD) {
-      const int nd = expand<K>(L, D, cD, nD, lane);
-#pragma unroll
-      for (int q = 0; q < K - 1; ++q) {
-        if (q == D) cur[q] = cD;
-        if (q == D + 1) { n[q] = nd; cur[q] = 0; }
-      }
-      ++D;
     } else {
-      if (D == 0) break;
-      --D;
-    }
-  }
-  if constexpr (!FILL) {
+      if (!c) return;
+      int mem[K];
+      mem[0] = r;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) total += __shfl_xor(total, o, 64);
-    *used = wave_or(usedl);
-  }
-  return total;
-}
-
-template <int K>
-__global__ __launch_bounds__(CWG) void k5b_count(CliqueArgs A) {
-  __shared__ WaveLds<K> s_w[CNW];
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int w = blockIdx.x * CNW + wv;
-  if (w >= A.n_roots) return;
-  const RootInfo R = root_info(A, w);
-  if (!R.ok) return;   // wave-uniform; counts were zeroed
-  WaveLds<K>& L = s_w[wv];
-  neighbourhood<K>(A, R, lane, L);
-  uint64_t used = 0;
-  uint32_t cnt;
-  if constexpr (K == 2) {
-    used = L.pm[1];
-    cnt = (uint32_t)__popcll(used);
-  } else {
-    cnt = root_cliques<K, false>(A, R, lane, L, &used, 0);
-  }
-  if (lane == 0) {
-    A.ccount[R.r] = (int32_t)cnt;
-    if (cnt) A.in_clique[R.r] = 1;
-  }
-  if (lane < R.d && ((used >> lane) & 1)) A.in_clique[L.nb[lane]] = 1;
-}
-
-template <int K>
-__global__ __launch_bounds__(CWG) void k5b_fill(CliqueArgs A) {
-  __shared__ WaveLds<K> s_w[CNW];
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int w = blockIdx.x * CNW + wv;
-  if (w >= A.n_roots) return;
-  const RootInfo R = root_info(A, w);
-  if (!R.ok) return;
-  WaveLds<K>& L = s_w[wv];
-  neighbourhood<K>(A, R, lane, L);
-  const int64_t out0 = A.clique_off[R.r];
-  if constexpr (K == 2) {
-    const uint64_t c = L.pm[1];
-    if ((c >> lane) & 1) {
-      const int64_t j = out0 + __popcll(c & ((1ull << lane) - 1));
-      A.members[j * 2] = R.r;
-      A.members[j * 2 + 1] = L.nb[lane];
+      for (int q = 0; q < K - 2; ++q) mem[q + 1] = A.e_dst[lo + ((P >> (6 * q)) & 63)];
+      int64_t j = L.off[i];
+      while (c) {
+        const int v = __builtin_ctzll(c);
+        c &= c - 1;
+        mem[K - 1] = A.e_dst[lo + v];
+#pragma unroll
+        for (int q = 0; q < K; ++q) A.members[j * K + q] = mem[q];
+        ++j;
+      }
     }
-  } else {
-    uint64_t used;
-    root_cliques<K, true>(A, R, lane, L, &used, out0);
+    return;
   }
+  const uint64_t pa = picker_lanes(rb, D + 2);
+  if (!FILL) {
+    int n = 0;
+    while (c) {
+      const int v = __builtin_ctzll(c);
+      c &= c - 1;
+      n += (M & A.adjg[lo + v] & pa) ? 1 : 0;
+    }
+    L.cnt[i] = n;
+  } else {
+    int64_t o = L.off[i];
+    while (c) {
+      const int v = __builtin_ctzll(c);
+      c &= c - 1;
+      const uint64_t m2 = M & A.adjg[lo + v];
+      if (m2 & pa) {
+        L.out_root[o] = r;
+        L.out_M[o] = m2;
+        L.out_P[o] = P | ((uint64_t)v << (6 * D));
+        ++o;
+      }
+    }
+  }
+}
+
+// Per-micrograph clique range.  Level-route cliques [0, C1) are sorted by root (box index, so
+// by micrograph): binary search for the micrograph's first and last picker-0 box.  DFS-route
+// micrographs: their roots' scanned offsets after C1.
+__global__ __launch_bounds__(WG) void k5_ranges(CliqueArgs A, int64_t C1, int64_t* rlo,
+                                               int64_t* rhi) {
+  const int m = blockIdx.x * WG + threadIdx.x;
+  if (m >= A.n_mg) return;
+  const int g0 = A.box_off[m * A.k], g1 = A.box_off[m * A.k + 1];
+  if (A.dfs_mg[m]) {
+    rlo[m] = C1 + A.clique_off[g0];
+    rhi[m] = C1 + A.clique_off[g1];
+    return;
+  }
+  int64_t b[2];
+  const int key[2] = {g0, g1};
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    int64_t a = 0, z = C1;
+    while (a < z) {
+      const int64_t mid = (a + z) >> 1;
+      if (A.members[mid * A.k] < key[t]) a = mid + 1; else z = mid;
+    }
+    b[t] = a;
+  }
+  rlo[m] = b[0];
+  rhi[m] = b[1];
 }
 
 // ILP epilogue, one thread per clique (get_cliques.py:164-202): COO rows (vertex ranks by
@@ -462,33 +365,67 @@ __global__ __launch_bounds__(WG) void k5_epilogue(CliqueArgs A) {
   A.consensus[j] = cons;
 }
 
+
 template <int K>
-static void launch_cliques_k(hipStream_t stream, int phase, int N, const CliqueArgs& A) {
-  if (phase == 0 || phase == 1) {
-    const int nb = (A.n_roots + CNW - 1) / CNW;
-    if (nb > 0) {
-      if (phase == 0) hipLaunchKernelGGL((k5b_count<K>), dim3(nb), dim3(CWG), 0, stream, A);
-      else hipLaunchKernelGGL((k5b_fill<K>), dim3(nb), dim3(CWG), 0, stream, A);
-    }
-    launch_cliques_dfs(stream, phase == 1, N, A);
+static int launch_level_k(hipStream_t stream, bool first, bool leaf, bool fill, const CliqueArgs& A,
+                          const LevelArgs& L) {
+  const int64_t nb = (L.n_items + WG - 1) / WG;
+  if (nb <= 0) return 0;
+#define RGC_LVL(F, LF, FL) \
+  hipLaunchKernelGGL((k5l<K, F, LF, FL>), dim3(nb), dim3(WG), 0, stream, A, L)
+  if (first) {
+    if (leaf) { if (fill) RGC_LVL(true, true, true); else RGC_LVL(true, true, false); }
+    else { if (fill) RGC_LVL(true, false, true); else RGC_LVL(true, false, false); }
   } else {
-    const int64_t nb = (A.C + WG - 1) / WG;
-    if (nb > 0) hipLaunchKernelGGL((k5_epilogue<K>), dim3(nb), dim3(WG), 0, stream, A);
+    if (leaf) { if (fill) RGC_LVL(false, true, true); else RGC_LVL(false, true, false); }
+    else { if (fill) RGC_LVL(false, false, true); else RGC_LVL(false, false, false); }
+  }
+#undef RGC_LVL
+  return 0;
+}
+
+int launch_clique_level(hipStream_t stream, bool first, bool leaf, bool fill, const CliqueArgs& A,
+                        const LevelArgs& L) {
+  switch (A.k) {
+    case 2: return launch_level_k<2>(stream, first, leaf, fill, A, L);
+    case 3: return launch_level_k<3>(stream, first, leaf, fill, A, L);
+    case 4: return launch_level_k<4>(stream, first, leaf, fill, A, L);
+    case 5: return launch_level_k<5>(stream, first, leaf, fill, A, L);
+    case 6: return launch_level_k<6>(stream, first, leaf, fill, A, L);
+    case 7: return launch_level_k<7>(stream, first, leaf, fill, A, L);
+    case 8: return launch_level_k<8>(stream, first, leaf, fill, A, L);
+    default: return -1;
   }
 }
 
-int launch_cliques(hipStream_t stream, int phase, int N, const CliqueArgs& A) {
+void launch_clique_setup(hipStream_t stream, int N, const CliqueArgs& A) {
+  const int nb = (N + WG - 1) / WG;
+  if (!nb) return;
+  hipLaunchKernelGGL(k5_route, dim3(nb), dim3(WG), 0, stream, N, A);
+  const int nr = A.n_roots;
+  if (!nr) return;
+  hipLaunchKernelGGL(k5n_build<16>, dim3((nr + WG / 16 - 1) / (WG / 16)), dim3(WG), 0, stream, N, A);
+  hipLaunchKernelGGL(k5n_build<64>, dim3((nr + WG / 64 - 1) / (WG / 64)), dim3(WG), 0, stream, N, A);
+}
+
+int launch_clique_epilogue(hipStream_t stream, const CliqueArgs& A) {
+  const int64_t nb = (A.C + WG - 1) / WG;
+  if (nb <= 0) return 0;
   switch (A.k) {
-    case 2: launch_cliques_k<2>(stream, phase, N, A); break;
-    case 3: launch_cliques_k<3>(stream, phase, N, A); break;
-    case 4: launch_cliques_k<4>(stream, phase, N, A); break;
-    case 5: launch_cliques_k<5>(stream, phase, N, A); break;
-    case 6: launch_cliques_k<6>(stream, phase, N, A); break;
-    case 7: launch_cliques_k<7>(stream, phase, N, A); break;
-    case 8: launch_cliques_k<8>(stream, phase, N, A); break;
+#define RGC_EPI(KK) \
+  case KK: hipLaunchKernelGGL((k5_epilogue<KK>), dim3(nb), dim3(WG), 0, stream, A); break;
+    RGC_EPI(2) RGC_EPI(3) RGC_EPI(4) RGC_EPI(5) RGC_EPI(6) RGC_EPI(7) RGC_EPI(8)
+#undef RGC_EPI
     default: return -1;
   }
   return 0;
+}
+
+void launch_clique_ranges(hipStream_t stream, const CliqueArgs& A, int64_t C1, int64_t* rlo,
+                          int64_t* rhi) {
+  if (A.n_mg > 0)
+    hipLaunchKernelGGL(k5_ranges, dim3((A.n_mg + WG - 1) / WG), dim3(WG), 0, stream, A, C1, rlo,
+                       rhi);
 }
 
 }  // namespace rgc

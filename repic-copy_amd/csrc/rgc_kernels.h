@@ -106,7 +106,7 @@ void launch_dump_edges(hipStream_t stream, int N, const int64_t* fwd_off, const 
 
 // Clique stage of the large-micrograph route (rgc_cliques.hip + the DFS fallback in
 // rgc_kernels.hip).  Boxes are sub-batch indices; outputs are offset by the caller.
-constexpr int RB_W = 64;   // bitmap width: roots with <= RB_W forward neighbours use a wavefront
+constexpr int RB_W = 64;   // bitmap width: roots with <= RB_W forward neighbours (level kernels)
 
 struct CliqueArgs {
   int k;
@@ -131,6 +131,11 @@ struct CliqueArgs {
   const int32_t* vrow;
   int32_t* ccount;
   uint8_t* in_clique;
+  uint64_t* adjg;            // [E] neighbourhood adjacency row of each root's i-th neighbour
+  uint64_t* rbound;          // [N] picker run starts in each root's neighbourhood (bytes)
+  uint8_t* rflag;            // [N] root enumerated by the level kernels
+  uint8_t* dfs_mg;           // [n_mg] micrograph takes the DFS route (a root > RB_W nbrs)
+  int64_t dfs_base;          // first output clique of the DFS route
   int32_t* members;
   int32_t* rows;
   float* w;
@@ -157,14 +162,29 @@ void launch_cc(hipStream_t stream, int phase, int N, int n_mg, int k, int get_cc
                const int64_t* fwd_off, const int32_t* e_dst, int32_t* parent, uint8_t* has_edge,
                int32_t* csize, MgStat* st, unsigned long long* ins_key,
                unsigned long long* comp_min);
-// phase 0: count cliques per root + mark clique vertices; 1: write members; 2: ILP epilogue
-int launch_cliques(hipStream_t stream, int phase, int N, const CliqueArgs& A);
+// One level of the prefix expansion (rgc_cliques.hip): level-D prefixes in, children out.
+struct LevelArgs {
+  int D;                     // members chosen so far (pickers 1..D)
+  int64_t n_items;           // prefixes (FIRST level: N boxes)
+  const int32_t* in_root;
+  const uint64_t* in_M;
+  const uint64_t* in_P;
+  int32_t* cnt;              // count pass: children (or cliques) per prefix
+  const int64_t* off;        // fill pass: scanned offsets
+  int32_t* out_root;
+  uint64_t* out_M;
+  uint64_t* out_P;
+};
+
+void launch_clique_setup(hipStream_t stream, int N, const CliqueArgs& A);
+int launch_clique_level(hipStream_t stream, bool first, bool leaf, bool fill, const CliqueArgs& A,
+                        const LevelArgs& L);
+int launch_clique_epilogue(hipStream_t stream, const CliqueArgs& A);
+void launch_clique_ranges(hipStream_t stream, const CliqueArgs& A, int64_t C1, int64_t* rlo,
+                          int64_t* rhi);
 int launch_cliques_dfs(hipStream_t stream, bool fill, int N, const CliqueArgs& A);
 void launch_rank(hipStream_t stream, int N, int n_mg, int k, const int32_t* box_off,
                  const int32_t* bmg, const MgGrid* grid, const double* x, const double* y,
                  const uint8_t* in_clique, int32_t* bcnt, int32_t* bslot, int64_t* boff,
                  int64_t* tile_buf, int64_t* total, int32_t* vsort, int32_t* vrow, MgStat* st);
-void launch_mg_offsets(hipStream_t stream, int n_mg, int k, const int32_t* box_off,
-                       const int64_t* coff, int64_t* mg_off);
-
 }  // namespace rgc

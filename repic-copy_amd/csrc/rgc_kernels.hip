@@ -7,8 +7,8 @@
 //   k2_pairs<FILL>    calc_jaccard (:40-46) + |dx| <= B prefilter + JI > 0.3 (:64-65,:138),
 //                     two-phase count -> scan -> fill; forward CSR sorted by target box
 //   k4_*              nx.connected_components stats (:145-149), --get_cc (:151-156)
-//   k5_cliques<K,..>  find_cliques (:49-56) for roots with more than RB_W forward
-//                     neighbours (the wavefront bitmap kernels of rgc_cliques.hip take the
+//   k5_cliques<K,..>  find_cliques (:49-56) for micrographs with a root of more than RB_W
+//                     forward neighbours (the level kernels of rgc_cliques.hip take the
 //                     rest; the ILP epilogue is k5_epilogue there)
 //   k7_*              row index v.index() (:164,:193) as a per-micrograph rank by
 //                     (x, y, id): x-bucket count -> scan -> scatter -> rank
@@ -418,12 +418,12 @@ __global__ __launch_bounds__(WG) void k4_target(int k, const int32_t* __restrict
 }
 
 // ----------------------------------------------------------------------------- K5 fallback
-// Roots whose forward neighbourhood exceeds the bitmap width of the wavefront kernels
-// (rgc_cliques.hip, RB_W boxes) are enumerated here, one thread per root, depth-first over the
-// global forward CSR (sorted-list membership by binary search).  COUNT: cliques per root and
-// the clique-vertex flags; FILL: the members of each clique at the root's scanned offset (the
-// ILP epilogue is the shared thread-per-clique kernel).  Lexicographic order, like the
-// wavefront kernels.
+// Micrographs with a root whose forward neighbourhood exceeds the bitmap width of the level
+// kernels (rgc_cliques.hip, RB_W boxes) are enumerated here, one thread per root,
+// depth-first over the global forward CSR (sorted-list membership by binary search).  COUNT:
+// cliques per root and the clique-vertex flags; FILL: the members of each clique at the
+// root's scanned offset after the level route's cliques (the ILP epilogue is the shared
+// thread-per-clique kernel).  Lexicographic order, like the level kernels.
 __device__ __forceinline__ int64_t lower_bound(const int32_t* a, int64_t lo, int64_t hi, int v) {
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
@@ -484,15 +484,15 @@ __global__ __launch_bounds__(WG) void k5_cliques(int N, CliqueArgs A) {
   const int g = blockIdx.x * WG + threadIdx.x;
   if (g >= N) return;
   if (A.bpick[g] != 0) return;
-  const int64_t d = A.fwd_off[g + 1] - A.fwd_off[g];
-  if (d <= RB_W) return;   // the wavefront kernels' root
   const int m = A.bmg[g];
+  if (!A.dfs_mg[m]) return;   // the level kernels' micrograph
+  if (A.fwd_off[g] == A.fwd_off[g + 1]) return;
   const MgStat s = A.st[m];
   if (s.status != 0) return;
   if ((A.flags & 1) && A.parent[g] != s.target) return;
   Walk<K> W;
   W.count = 0;
-  W.out = FILL ? A.clique_off[g] : 0;
+  W.out = FILL ? A.dfs_base + A.clique_off[g] : 0;
 #pragma unroll
   for (int i = 0; i <= K; ++i) W.pb[i] = A.box_off[m * A.k + i];
   W.mem[0] = g;
@@ -566,14 +566,6 @@ __global__ __launch_bounds__(WG) void k7_nvert(int n_mg, int k, const int32_t* _
   const int m = blockIdx.x * WG + threadIdx.x;
   if (m >= n_mg) return;
   st[m].n_vert = (int)(boff[box_off[m * k + k]] - boff[box_off[m * k]]);
-}
-
-__global__ __launch_bounds__(WG) void k_mg_offsets(int n_mg, int k, const int32_t* __restrict__ box_off,
-                                                   const int64_t* __restrict__ coff,
-                                                   int64_t* mg_off) {
-  const int m = blockIdx.x * WG + threadIdx.x;
-  if (m > n_mg) return;
-  mg_off[m] = coff[box_off[m * k]];
 }
 
 // ----------------------------------------------------------------------------- sub-batch
@@ -737,11 +729,6 @@ void launch_rank(hipStream_t stream, int N, int n_mg, int k, const int32_t* box_
                vsort, vrow);
   }
   RGC_LAUNCH(k7_nvert, (n_mg + WG - 1) / WG, WG, n_mg, k, box_off, boff, st);
-}
-
-void launch_mg_offsets(hipStream_t stream, int n_mg, int k, const int32_t* box_off,
-                       const int64_t* coff, int64_t* mg_off) {
-  RGC_LAUNCH(k_mg_offsets, (n_mg + 1 + WG - 1) / WG, WG, n_mg, k, box_off, coff, mg_off);
 }
 
 }  // namespace rgc
