@@ -58,7 +58,7 @@ enum DevBufId {
   D_SUBMG, D_SUBX, D_SUBY, D_SUBS, D_ORIG, D_STAMPS,
   D_BOXOFF, D_CELLOFF, D_P0OFF, D_IDBASE, D_GRID, D_CELLSTART, D_SX, D_SY, D_SBOX, D_SPICK, D_SMG, D_BMG,
   D_BPICK, D_FWDCNT, D_FWDOFF, D_TILES, D_TOTAL, D_EDST, D_EJI, D_PARENT, D_HASEDGE, D_CSIZE,
-  D_STAT, D_INSKEY, D_COMPMIN, D_CCOUNT, D_COFF, D_INCL, D_VLIST, D_VSORT, D_VROW, D_BOFF, D_RLO, D_ADJG, D_RBOUND, D_RFLAG, D_DFSMG,
+  D_STAT, D_INSKEY, D_COMPMIN, D_CCOUNT, D_COFF, D_INCL, D_VLIST, D_VSORT, D_VROW, D_BOFF, D_RLO, D_ADJG, D_RBOUND, D_RFLAG, D_DFSMG, D_ROOTBOX, D_EXLIST,
   D_LCNT, D_LOFF, D_LROOT0, D_LROOT1, D_LM0, D_LM1, D_LP0, D_LP1,
   // RGC_F_EDGES test hook
   D_EU, D_EV, D_EJIOUT,
@@ -305,6 +305,7 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   TRY(ensure_host(c, H_MGOFF, 2 * (size_t)n_mg * 8 + 8));
   TRY(ensure_dev(c, D_RBOUND, N * 8));
   TRY(ensure_dev(c, D_RFLAG, N));
+  TRY(ensure_dev(c, D_ROOTBOX, n_roots * 4));
   TRY(ensure_dev(c, D_DFSMG, n_mg));
 
   hipStream_t s = c->stream;
@@ -377,6 +378,8 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   A.ccount = D<int32_t>(c, D_CCOUNT); A.in_clique = D<uint8_t>(c, D_INCL);
   A.adjg = D<uint64_t>(c, D_ADJG); A.rbound = D<uint64_t>(c, D_RBOUND);
   A.rflag = D<uint8_t>(c, D_RFLAG); A.dfs_mg = D<uint8_t>(c, D_DFSMG); A.dfs_base = 0;
+  A.root_box = D<int32_t>(c, D_ROOTBOX);
+  A.exlist = nullptr; A.excount = nullptr;
   A.members = nullptr; A.rows = nullptr; A.w = nullptr; A.conf = nullptr; A.consensus = nullptr;
   A.order = nullptr;
   int64_t* d_tot = D<int64_t>(c, D_TOTAL);   // [0] edges, [1] DFS cliques, [2] level, [3] rank
@@ -449,6 +452,10 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   launch_clique_level(s, k == 2, true, true, A, L);
   TRY(mark(c, "k5_dfs_fill"));
   launch_cliques_dfs(s, true, (int)N, A);
+  TRY(ensure_dev(c, D_EXLIST, C * 8));
+  A.exlist = D<int64_t>(c, D_EXLIST);
+  A.excount = reinterpret_cast<unsigned long long*>(d_tot + 3);   // rank scan total is dead
+  HIPCHK(hipMemsetAsync(A.excount, 0, 8, s));
   TRY(mark(c, "k5_epilogue"));
   launch_clique_epilogue(s, A);
   TRY(mark(c, "k5_ranges"));

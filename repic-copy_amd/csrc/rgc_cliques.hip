@@ -6,10 +6,10 @@
 // one-box-per-picker k-tuples that are pairwise adjacent.  Every such tuple has one picker-0
 // member, its "root"; the other k-1 members are forward neighbours of the root.
 //
-// 1. Neighbourhood bitmaps (k5n_build): a group of G lanes per root (G = 16: four roots per
-//    wavefront; G = 64 for roots with 17..64 forward neighbours).  Lane i holds the i-th
-//    forward neighbour (sorted by box index, so each picker is a contiguous run of lanes);
-//    its adjacency row inside the neighbourhood (a 64-bit mask, forward edges only) goes to
+// 1. Neighbourhood bitmaps (k5n_build): a group of 16 lanes per root (four roots per
+//    wavefront), lane l holding the root's forward neighbours l, l + 16, ... (sorted by box
+//    index, so each picker is a contiguous run of neighbour indices).  The adjacency row of
+//    neighbour i inside the neighbourhood (a 64-bit mask, forward edges only) goes to
 //    adjg[fwd_off[root] + i] and the picker run starts to rbound[root].
 // 2. Level-synchronous prefix expansion over the whole sub-batch (k5l<K, ...>): a level-D
 //    prefix = (root, mask M of neighbourhood lanes adjacent to all chosen members, chosen
@@ -29,6 +29,7 @@
 #include "rgc_device.h"
 #include "rgc_kernels.h"
 
+#include <algorithm>
 #include <climits>
 
 namespace rgc {
@@ -51,75 +52,82 @@ __device__ __forceinline__ bool root_valid(const CliqueArgs& A, int g, int m) {
   return s.status == 0 && (!(A.flags & 1) || A.parent[g] == s.target);
 }
 
-// micrographs with a root of more than RB_W forward neighbours take the DFS route
+// Thread per box: the root list (wavefront-free indexing of picker-0 boxes) and the route of
+// each micrograph (DFS when a root has more than RB_W forward neighbours).
 __global__ __launch_bounds__(WG) void k5_route(int N, CliqueArgs A) {
   const int g = blockIdx.x * WG + threadIdx.x;
-  if (g >= N) return;
+  if (g >= N || A.bpick[g] != 0) return;
   const int m = A.bmg[g];
+  A.root_box[A.p0off[m] + (g - A.box_off[m * A.k])] = g;
   if (root_valid(A, g, m) && A.fwd_off[g + 1] - A.fwd_off[g] > RB_W) A.dfs_mg[m] = 1;
 }
 
-template <int G>
-__global__ __launch_bounds__(WG) void k5n_build(int, CliqueArgs A) {
-  constexpr int NG = WG / G;
-  __shared__ int32_t s_nb[NG][G];
-  const int grp = threadIdx.x / G, lane = threadIdx.x % G;
+// Neighbourhood bitmaps, NBG lanes per root; lane l holds neighbours l, l + NBG, ...
+constexpr int NBG = 16;
+constexpr int NBQ = RB_W / NBG;
+
+__global__ __launch_bounds__(WG) void k5n_build(CliqueArgs A) {
+  constexpr int NG = WG / NBG;
+  __shared__ int32_t s_nb[NG][RB_W];
+  const int grp = threadIdx.x / NBG, lane = threadIdx.x % NBG;
   const int w = blockIdx.x * NG + grp;   // one group per picker-0 box
   if (w >= A.n_roots) return;
-  int m = 0;
-  {
-    int hi = A.n_mg;
-    while (hi - m > 1) {
-      const int mid = (m + hi) >> 1;
-      if (A.p0off[mid] <= w) m = mid; else hi = mid;
-    }
-  }
-  const int g = A.box_off[m * A.k] + (w - A.p0off[m]);
+  const int g = A.root_box[w];
+  const int m = A.bmg[g];
   if (!root_valid(A, g, m) || A.dfs_mg[m]) return;
   const int64_t lo = A.fwd_off[g];
   const int d = (int)(A.fwd_off[g + 1] - lo);
-  if (d > G || (G > 16 && d <= 16)) return;   // the other launch's root
   int32_t* nb = s_nb[grp];
-  int u = -1, pk = A.k;
-  if (lane < d) {
-    u = A.e_dst[lo + lane];
-    pk = A.bpick[u];
-    nb[lane] = u;
+  int u[NBQ], pk[NBQ];
+#pragma unroll
+  for (int q = 0; q < NBQ; ++q) {
+    const int i = lane + q * NBG;
+    u[q] = -1;
+    pk[q] = A.k;
+    if (i < d) {
+      u[q] = A.e_dst[lo + i];
+      pk[q] = A.bpick[u[q]];
+      nb[i] = u[q];
+    }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  if (lane < d) {
+  const int last = nb[d - 1];
+#pragma unroll
+  for (int q = 0; q < NBQ; ++q) {
+    const int i = lane + q * NBG;
+    if (i >= d) break;
     // adjacency row: u's forward targets looked up in the sorted neighbourhood (only lanes
     // after u can match); four loads in flight per step
     uint64_t mask = 0;
-    const int64_t e0 = A.fwd_off[u], e1 = A.fwd_off[u + 1];
-    const int last = nb[d - 1];
+    const int64_t e0 = A.fwd_off[u[q]], e1 = A.fwd_off[u[q] + 1];
     for (int64_t e = e0; e < e1; e += 4) {
       int t[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) t[q] = e + q < e1 ? A.e_dst[e + q] : INT_MAX;
+      for (int z = 0; z < 4; ++z) t[z] = e + z < e1 ? A.e_dst[e + z] : INT_MAX;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (t[q] > last) continue;
-        int a = lane + 1, b = d;   // first lane with nb >= t
+      for (int z = 0; z < 4; ++z) {
+        if (t[z] > last) continue;
+        int a = i + 1, b = d;   // first lane with nb >= t
         while (a < b) {
           const int mid = (a + b) >> 1;
-          if (nb[mid] < t[q]) a = mid + 1; else b = mid;
+          if (nb[mid] < t[z]) a = mid + 1; else b = mid;
         }
-        if (a < d && nb[a] == t[q]) mask |= 1ull << a;
+        if (a < d && nb[a] == t[z]) mask |= 1ull << a;
       }
       if (t[3] >= last) break;
     }
-    A.adjg[lo + lane] = mask;
+    A.adjg[lo + i] = mask;
   }
   // picker runs: lanes are sorted picker-major, so the first lane of picker p = #lanes below p
-  const uint64_t gmask = (G == 64 ? ~0ull : (((1ull << G) - 1) << ((threadIdx.x & 63) / G * G)));
+  const uint64_t gmask = ((1ull << NBG) - 1) << ((threadIdx.x & 63) / NBG * NBG);
   uint64_t rb = 0;
 #pragma unroll
   for (int p = 1; p < MAX_K; ++p) {
-    const uint64_t below = __ballot(lane < d && pk < p) & gmask;
-    const int s = __popcll(below);
+    int s = 0;
+#pragma unroll
+    for (int q = 0; q < NBQ; ++q) s += __popcll(__ballot(pk[q] < p) & gmask);
     if (p < A.k) rb |= (uint64_t)s << (8 * (p - 1));
   }
   rb |= (uint64_t)d << (8 * (A.k - 1));
@@ -248,25 +256,30 @@ __global__ __launch_bounds__(WG) void k5_epilogue(CliqueArgs A) {
   int mem[K];
 #pragma unroll
   for (int i = 0; i < K; ++i) mem[i] = A.members[j * K + i];
-  double xs[K], ys[K], s[K];
-  int r[K];
+  double xs[K], ys[K];
+  float conf32;
+  {
+    double s[K];
+    int r[K];
 #pragma unroll
-  for (int i = 0; i < K; ++i) {
-    xs[i] = A.x[mem[i]];
-    ys[i] = A.y[mem[i]];
-    s[i] = A.score[mem[i]];
-    r[i] = A.vrow[mem[i]];
-  }
-#pragma unroll
-  for (int i = 0; i < K; ++i)
-#pragma unroll
-    for (int q = 0; q < K - 1 - i; ++q) {
-      const int a = r[q], b = r[q + 1];
-      r[q] = min(a, b);
-      r[q + 1] = max(a, b);
+    for (int i = 0; i < K; ++i) {
+      xs[i] = A.x[mem[i]];
+      ys[i] = A.y[mem[i]];
+      s[i] = A.score[mem[i]];
+      r[i] = A.vrow[mem[i]];
     }
 #pragma unroll
-  for (int i = 0; i < K; ++i) A.rows[j * K + i] = r[i];
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+      for (int q = 0; q < K - 1 - i; ++q) {
+        const int a = r[q], b = r[q + 1];
+        r[q] = min(a, b);
+        r[q + 1] = max(a, b);
+      }
+#pragma unroll
+    for (int i = 0; i < K; ++i) A.rows[j * K + i] = r[i];
+    conf32 = (float)median_n<K>(s);   // conf = f32(median score)
+  }
   const double B = A.B, two_b2 = A.two_b2;
   double I[NE];   // member-pair overlaps (a < b), reference op order
   {
@@ -276,31 +289,6 @@ __global__ __launch_bounds__(WG) void k5_epilogue(CliqueArgs A) {
 #pragma unroll
       for (int b = a + 1; b < K; ++b) I[t++] = overlap(xs[a], ys[a], xs[b], ys[b], B);
   }
-  // conf = f32(median score); median JI = JI of the median overlap (JI is non-decreasing in
-  // I and the f64 quotient keeps that order), so one or two reference divisions
-  double sc[K];
-#pragma unroll
-  for (int i = 0; i < K; ++i) sc[i] = s[i];
-  const float conf32 = (float)median_n<K>(sc);
-  double med;
-  {
-    double Is[NE];
-#pragma unroll
-    for (int t = 0; t < NE; ++t) Is[t] = I[t];
-    if (NE & 1) {
-      med = median_n<NE>(Is);
-      med = med / (two_b2 - med);
-    } else {
-      bool nan = false;
-#pragma unroll
-      for (int t = 0; t < NE; ++t) nan |= isnan(Is[t]);
-      sort_n<NE>(Is);
-      const double a = Is[NE / 2 - 1], b = Is[NE / 2];
-      med = nan ? NAN : ((a / (two_b2 - a)) + (b / (two_b2 - b))) / 2.0;
-    }
-  }
-  A.w[j] = (float)((double)conf32 * med);
-  A.conf[j] = conf32;
   const bool multi = (A.flags & 2) != 0;
   int arg = 0;
   bool exact = multi;
@@ -330,7 +318,51 @@ __global__ __launch_bounds__(WG) void k5_epilogue(CliqueArgs A) {
     }
     exact = !(d1 - d2 > 1e-5f);
   }
+  // median JI = JI of the median overlap (JI is non-decreasing in I and the f64 quotient
+  // keeps that order): one or two reference divisions; I is sorted in place
+  double med;
+  if (NE & 1) {
+    med = median_n<NE>(I);
+    med = med / (two_b2 - med);
+  } else {
+    bool nan = false;
+#pragma unroll
+    for (int t = 0; t < NE; ++t) nan |= isnan(I[t]);
+    sort_n<NE>(I);
+    const double a = I[NE / 2 - 1], b = I[NE / 2];
+    med = nan ? NAN : ((a / (two_b2 - a)) + (b / (two_b2 - b))) / 2.0;
+  }
+  A.w[j] = (float)((double)conf32 * med);
+  A.conf[j] = conf32;
   if (exact) {
+    // the rare cliques that need exact f64 degrees / node order: second kernel (its 64-bit
+    // hashing and K x K JIs stay out of this kernel's register budget)
+    A.exlist[atomicAdd(A.excount, 1ull)] = j;
+    return;
+  }
+  int cons = mem[0];
+#pragma unroll
+  for (int i = 1; i < K; ++i) cons = (arg == i) ? mem[i] : cons;
+  A.consensus[j] = cons;
+}
+
+// Consensus (and --multi_out node order) of the cliques k5_epilogue deferred: exact f64
+// weighted degrees (get_cliques.py:182-183) and, on ties, the first tied member in networkx's
+// node-iteration order (CPython set order of (x, y, id), or graph insertion order when
+// 2k >= |G|).  Grid-stride over the deferred list.
+template <int K>
+__global__ __launch_bounds__(WG) void k5_epi_exact(CliqueArgs A) {
+  const int64_t n = (int64_t)*A.excount;
+  for (int64_t t = (int64_t)blockIdx.x * WG + threadIdx.x; t < n; t += (int64_t)gridDim.x * WG) {
+    const int64_t j = A.exlist[t];
+    int mem[K];
+    double xs[K], ys[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      mem[i] = A.members[j * K + i];
+      xs[i] = A.x[mem[i]];
+      ys[i] = A.y[mem[i]];
+    }
     const int m = A.bmg[mem[0]];
     const int64_t idb = A.id_base[m] - (int64_t)A.box_off[m * A.k];
     double ji[K][K];
@@ -340,7 +372,7 @@ __global__ __launch_bounds__(WG) void k5_epilogue(CliqueArgs A) {
     for (int a = 0; a < K; ++a) {
       ids[a] = idb + mem[a];
 #pragma unroll
-      for (int b = a + 1; b < K; ++b) ji[a][b] = jaccard(xs[a], ys[a], xs[b], ys[b], B, two_b2);
+      for (int b = a + 1; b < K; ++b) ji[a][b] = jaccard(xs[a], ys[a], xs[b], ys[b], A.B, A.two_b2);
     }
     const bool set_order = 2 * K < A.st[m].n_nodes;
     if (!set_order) {
@@ -348,8 +380,9 @@ __global__ __launch_bounds__(WG) void k5_epilogue(CliqueArgs A) {
       for (int i = 0; i < K; ++i) ins[i] = A.ins_key[mem[i]];
     }
     uint32_t top;
-    arg = epi_degree_max<K>(ji, &top);
+    int arg = epi_degree_max<K>(ji, &top);
     const bool tie = (top & (top - 1)) != 0;
+    const bool multi = (A.flags & 2) != 0;
     if (tie || multi) {
       const uint32_t ord = node_order<K>(mem, xs, ys, ids, set_order, ins);
       if (tie) arg = epi_tie_arg<K>(top, ord);
@@ -358,13 +391,12 @@ __global__ __launch_bounds__(WG) void k5_epilogue(CliqueArgs A) {
         for (int i = 0; i < K; ++i) A.order[j * K + i] = (uint8_t)((ord >> (4 * i)) & 15);
       }
     }
-  }
-  int cons = mem[0];
+    int cons = mem[0];
 #pragma unroll
-  for (int i = 1; i < K; ++i) cons = (arg == i) ? mem[i] : cons;
-  A.consensus[j] = cons;
+    for (int i = 1; i < K; ++i) cons = (arg == i) ? mem[i] : cons;
+    A.consensus[j] = cons;
+  }
 }
-
 
 template <int K>
 static int launch_level_k(hipStream_t stream, bool first, bool leaf, bool fill, const CliqueArgs& A,
@@ -403,17 +435,19 @@ void launch_clique_setup(hipStream_t stream, int N, const CliqueArgs& A) {
   if (!nb) return;
   hipLaunchKernelGGL(k5_route, dim3(nb), dim3(WG), 0, stream, N, A);
   const int nr = A.n_roots;
-  if (!nr) return;
-  hipLaunchKernelGGL(k5n_build<16>, dim3((nr + WG / 16 - 1) / (WG / 16)), dim3(WG), 0, stream, N, A);
-  hipLaunchKernelGGL(k5n_build<64>, dim3((nr + WG / 64 - 1) / (WG / 64)), dim3(WG), 0, stream, N, A);
+  if (nr) hipLaunchKernelGGL(k5n_build, dim3((nr + WG / NBG - 1) / (WG / NBG)), dim3(WG), 0, stream, A);
 }
 
 int launch_clique_epilogue(hipStream_t stream, const CliqueArgs& A) {
   const int64_t nb = (A.C + WG - 1) / WG;
   if (nb <= 0) return 0;
   switch (A.k) {
-#define RGC_EPI(KK) \
-  case KK: hipLaunchKernelGGL((k5_epilogue<KK>), dim3(nb), dim3(WG), 0, stream, A); break;
+#define RGC_EPI(KK)                                                                     \
+  case KK:                                                                              \
+    hipLaunchKernelGGL((k5_epilogue<KK>), dim3(nb), dim3(WG), 0, stream, A);            \
+    hipLaunchKernelGGL((k5_epi_exact<KK>), dim3(std::min<int64_t>(nb, 1024)), dim3(WG), 0, \
+                       stream, A);                                                      \
+    break;
     RGC_EPI(2) RGC_EPI(3) RGC_EPI(4) RGC_EPI(5) RGC_EPI(6) RGC_EPI(7) RGC_EPI(8)
 #undef RGC_EPI
     default: return -1;

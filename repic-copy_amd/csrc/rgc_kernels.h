@@ -135,6 +135,9 @@ struct CliqueArgs {
   uint64_t* rbound;          // [N] picker run starts in each root's neighbourhood (bytes)
   uint8_t* rflag;            // [N] root enumerated by the level kernels
   uint8_t* dfs_mg;           // [n_mg] micrograph takes the DFS route (a root > RB_W nbrs)
+  int32_t* root_box;         // [n_roots] box of each picker-0 root
+  int64_t* exlist;           // [C] epilogue: cliques deferred to the exact pass
+  unsigned long long* excount;
   int64_t dfs_base;          // first output clique of the DFS route
   int32_t* members;
   int32_t* rows;
