@@ -80,6 +80,10 @@ struct Buf {
 constexpr int LDS_BLOCK = 1280;
 constexpr int LDS_BLOCKS = 128;
 constexpr int FUSED_WG = 512;
+// Micrographs above this many boxes go straight to the large-micrograph route: at ~4k boxes
+// the fused kernel's LDS leaves room for ~2 edges per box, fewer than crowded micrographs
+// have (C3: 3.8), so the fused attempt would only defer them after its pair pass.
+constexpr int64_t FUSED_MAX_BOXES = 3072;
 // device cursors after the per-micrograph block: [0] clique reservation, [1] edges of finished
 // micrographs, [2] edge-dump reservation (RGC_F_EDGES), [3] spare
 constexpr size_t CUR_BYTES = 32;
@@ -578,7 +582,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   std::vector<int32_t> todo0;
   auto mg_class = [&](int m) {
     const int64_t nm = in->box_off[(int64_t)(m + 1) * k] - in->box_off[(int64_t)m * k];
-    return nm <= 65535 ? fused_class(nm) : 0;
+    return nm <= FUSED_MAX_BOXES ? fused_class(nm) : 0;
   };
   // per-call plan lookup: few distinct classes, so a linear list beats the shared memo
   std::vector<std::pair<int, const FusedPlan*>> local_plans;
@@ -597,7 +601,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
     nmin = std::min(nmin, nm);
     nmaxb = std::max(nmaxb, nm);
   }
-  const bool all0 = !no_fused && n_mg > 0 && nmaxb <= 65535 &&
+  const bool all0 = !no_fused && n_mg > 0 && nmaxb <= FUSED_MAX_BOXES &&
                     plan_of(0, fused_class(nmaxb)).nmax &&
                     plan_of(0, fused_class(nmin)).wg == plan_of(0, fused_class(nmaxb)).wg;
   if (!all0) {
@@ -757,31 +761,44 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
     }
     sbo[(size_t)ns * k] = acc;
     for (size_t i = 0; i < sbo.size(); ++i) sbo32[i] = (int32_t)sbo[i];
-    TRY(ensure_dev(c, D_SUBMG, ns * 4));
-    TRY(ensure_dev(c, D_SUBX, acc * 8));
-    TRY(ensure_dev(c, D_SUBY, acc * 8));
-    TRY(ensure_dev(c, D_SUBS, acc * 8));
-    TRY(ensure_dev(c, D_ORIG, acc * 4));
-    TRY(ensure_dev(c, D_BOXOFF, sbo32.size() * 4));
-    HIPCHK(hipMemcpy(D<void>(c, D_SUBMG), deferred.data(), ns * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(D<void>(c, D_BOXOFF), sbo32.data(), sbo32.size() * 4, hipMemcpyHostToDevice));
-    TRY(mark(c, "k_gather"));
-    launch_gather(s, ns, k, D<int32_t>(c, D_SUBMG), d_bo, D<int32_t>(c, D_BOXOFF),
-                  x, y, sc, D<double>(c, D_SUBX), D<double>(c, D_SUBY), D<double>(c, D_SUBS),
-                  D<int32_t>(c, D_ORIG));
-    HIPCHK(hipStreamSynchronize(s));
+    // every micrograph deferred (a batch of large micrographs): the sub-batch IS the batch,
+    // no gather and no index remap
+    const bool ident = ns == n_mg;
+    const double *sx = x, *sy = y, *ss = sc;
+    const int32_t* orig = nullptr;
+    if (!ident) {
+      TRY(ensure_dev(c, D_SUBMG, ns * 4));
+      TRY(ensure_dev(c, D_SUBX, acc * 8));
+      TRY(ensure_dev(c, D_SUBY, acc * 8));
+      TRY(ensure_dev(c, D_SUBS, acc * 8));
+      TRY(ensure_dev(c, D_ORIG, acc * 4));
+      TRY(ensure_dev(c, D_BOXOFF, sbo32.size() * 4));
+      HIPCHK(hipMemcpy(D<void>(c, D_SUBMG), deferred.data(), ns * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(D<void>(c, D_BOXOFF), sbo32.data(), sbo32.size() * 4,
+                       hipMemcpyHostToDevice));
+      TRY(mark(c, "k_gather"));
+      launch_gather(s, ns, k, D<int32_t>(c, D_SUBMG), d_bo, D<int32_t>(c, D_BOXOFF),
+                    x, y, sc, D<double>(c, D_SUBX), D<double>(c, D_SUBY), D<double>(c, D_SUBS),
+                    D<int32_t>(c, D_ORIG));
+      HIPCHK(hipStreamSynchronize(s));
+      sx = D<double>(c, D_SUBX);
+      sy = D<double>(c, D_SUBY);
+      ss = D<double>(c, D_SUBS);
+      orig = D<int32_t>(c, D_ORIG);
+    }
     std::vector<MgStat> sst;
     int64_t Cm = 0, Em = 0;
-    TRY(run_multi(c, ns, k, B, two_b2, get_cc, multi, sbo.data(), sid.data(),
-                  D<double>(c, D_SUBX), D<double>(c, D_SUBY), D<double>(c, D_SUBS), fused_total, sst,
-                  &Cm, &Em));
-    TRY(mark(c, "k_remap"));
-    launch_remap(s, Cm, k, D<int32_t>(c, D_ORIG), D<int32_t>(c, D_CONS) + fused_total,
-                 D<int32_t>(c, D_MEMBERS) + fused_total * k);
+    TRY(run_multi(c, ns, k, B, two_b2, get_cc, multi, sbo.data(), sid.data(), sx, sy, ss,
+                  fused_total, sst, &Cm, &Em));
+    if (!ident) {
+      TRY(mark(c, "k_remap"));
+      launch_remap(s, Cm, k, orig, D<int32_t>(c, D_CONS) + fused_total,
+                   D<int32_t>(c, D_MEMBERS) + fused_total * k);
+    }
     if (want_edges) {
       TRY(ensure_edges(c, fused_edges + Em, fused_edges));
       launch_dump_edges(s, (int)acc, D<int64_t>(c, D_FWDOFF), D<int32_t>(c, D_EDST),
-                        D<double>(c, D_EJI), D<int32_t>(c, D_ORIG), D<int32_t>(c, D_EU) + fused_edges,
+                        D<double>(c, D_EJI), orig, D<int32_t>(c, D_EU) + fused_edges,
                         D<int32_t>(c, D_EV) + fused_edges, D<double>(c, D_EJIOUT) + fused_edges);
       fused_edges += Em;
     }

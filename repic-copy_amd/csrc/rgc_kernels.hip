@@ -604,8 +604,8 @@ __global__ __launch_bounds__(WG) void k_dump_edges(int N, const int64_t* __restr
   const int g = blockIdx.x * WG + threadIdx.x;
   if (g >= N) return;
   for (int64_t e = fwd_off[g]; e < fwd_off[g + 1]; ++e) {
-    eu[e] = orig[g];
-    ev[e] = orig[e_dst[e]];
+    eu[e] = orig ? orig[g] : g;
+    ev[e] = orig ? orig[e_dst[e]] : e_dst[e];
     eji[e] = e_ji[e];
   }
 }
