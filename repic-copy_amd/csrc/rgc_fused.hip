@@ -502,6 +502,10 @@ struct BfsOut {
   int lvl[K + 1];   // byte offset in q of each level's entries (2..K)
 };
 
+// REWALK (P6 re-run of a root chunk): the split array and the union-find parents are dead by
+// then, so first segments come from a binary search for the next picker's first position and
+// a root is valid iff it was marked as a clique vertex in P4 (it has a clique, which lies in
+// the --get_cc target component); vertices are already marked.
 template <int K, int D>
 struct BfsLevel {
   // prefix members of entry e of level D (D members, compile-time indices only)
@@ -519,8 +523,16 @@ struct BfsLevel {
     mm[0] = (int)cur;
   }
 
+  template <bool REWALK>
+  __device__ __forceinline__ static int seg_end(const FShared& S, const int (&pp)[K + 1], int m) {
+    if (REWALK) return lb16(S.dst, S.fwd[m], S.fwd[m + 1], pp[D + 1]);
+    return S.split[m];
+  }
+
+  template <bool REWALK>
   __device__ __forceinline__ static BfsOut<K> run(const FShared& S, FusedHdr& H, char* q,
-                                                  int qbytes, BfsOut<K>& out, int64_t nD, int tid) {
+                                                  int qbytes, BfsOut<K>& out, int64_t nD, int tid,
+                                                  const int (&pp)[K + 1]) {
     int (&lvl)[K + 1] = out.lvl;
     // temps of this level at the top of q
     const int tb = (qbytes - 8 * (int)(nD + 1)) & ~7;
@@ -531,7 +543,7 @@ struct BfsLevel {
       int mm[K];
       prefix(q, lvl, (uint32_t)e, mm);
       const int m = mm[D - 1];
-      const int lo = S.fwd[m], hi = S.split[m];
+      const int lo = S.fwd[m], hi = seg_end<REWALK>(S, pp, m);
       uint32_t mask = 0, cnt = 0;
       for (int t = lo; t < hi; ++t) {
         const int h = S.dst[t];
@@ -554,7 +566,7 @@ struct BfsLevel {
       int mm[K];
       prefix(q, lvl, (uint32_t)e, mm);
       const int m = mm[D - 1];
-      const int lo = S.fwd[m], hi = S.split[m];
+      const int lo = S.fwd[m], hi = seg_end<REWALK>(S, pp, m);
       const uint32_t mask = MK[e];
       uint32_t o = CN[e];
       for (int t = lo; t < hi; ++t) {
@@ -571,9 +583,11 @@ struct BfsLevel {
         if (!ok) continue;
         reinterpret_cast<uint32_t*>(q + nb)[o] = ((uint32_t)e << 16) | (uint32_t)h;
         if (last) {
+          if (!REWALK) {
 #pragma unroll
-          for (int d = 0; d < K - 1; ++d) S.flags[mm[d]] = 3;
-          S.flags[h] = 3;
+            for (int d = 0; d < K - 1; ++d) S.flags[mm[d]] = 3;
+            S.flags[h] = 3;
+          }
           reinterpret_cast<uint16_t*>(q + nb + 4 * (int)nN)[o] = 0;
         }
         ++o;
@@ -582,7 +596,7 @@ struct BfsLevel {
     __syncthreads();
     lvl[D + 1] = nb;
     if constexpr (D + 1 < K) {
-      return BfsLevel<K, D + 1>::run(S, H, q, qbytes, out, nN, tid);
+      return BfsLevel<K, D + 1>::template run<REWALK>(S, H, q, qbytes, out, nN, tid, pp);
     } else {
       out.C = nN;
       return out;
@@ -590,34 +604,50 @@ struct BfsLevel {
   }
 };
 
-template <int K>
+// Cliques of the roots [r0, r1) (picker-0 positions).  Returns C = -1 when a level does not
+// fit the queue region; the caller then retries with fewer roots (root chunks, P4) and falls
+// back to the per-root DFS only when a single root does not fit.
+template <int K, bool REWALK>
 __device__ __forceinline__ BfsOut<K> bfs_cliques(const FShared& S, FusedHdr& H, char* q,
-                                                 int qbytes, int n0, bool get_cc, uint32_t target,
-                                                 int tid) {
+                                                 int qbytes, int r0, int r1, bool get_cc,
+                                                 uint32_t target, int tid,
+                                                 const int (&pp)[K + 1]) {
   BfsOut<K> out;
   out.C = -1;
 #pragma unroll
   for (int d = 0; d <= K; ++d) out.lvl[d] = 0;
+  const int nr = r1 - r0;
+  auto root_ok = [&](int r) {
+    if (REWALK) return S.flags[r] == 3;
+    return S.fwd[r] < S.fwd[r + 1] && (!get_cc || S.parent[r] == target);
+  };
+  auto seg_end = [&](int r) {
+    if (REWALK) return lb16(S.dst, S.fwd[r], S.fwd[r + 1], pp[2]);
+    return (int)S.split[r];
+  };
   // level 1 -> 2: every root's first segment (picker-1 neighbours), no checks needed
   uint32_t* cnt = S.cnt;
-  for (int r = tid; r < n0; r += FWG) {
-    const bool ok = S.fwd[r] < S.fwd[r + 1] && (!get_cc || S.parent[r] == target);
-    cnt[r] = ok ? (uint32_t)(S.split[r] - S.fwd[r]) : 0u;
+  for (int i = tid; i < nr; i += FWG) {
+    const int r = r0 + i;
+    cnt[i] = root_ok(r) ? (uint32_t)(seg_end(r) - S.fwd[r]) : 0u;
   }
   __syncthreads();
-  const int64_t n2 = block_scan_array<FWG>(cnt, n0, H.red64);
+  const int64_t n2 = block_scan_array<FWG>(cnt, nr, H.red64);
   constexpr bool last = K == 2;
   if (n2 > 65535 || n2 * (last ? 6 : 4) > qbytes) return out;
-  for (int r = tid; r < n0; r += FWG) {
-    const bool ok = S.fwd[r] < S.fwd[r + 1] && (!get_cc || S.parent[r] == target);
-    if (!ok) continue;
-    uint32_t o = cnt[r];
-    for (int t = S.fwd[r]; t < S.split[r]; ++t, ++o) {
+  for (int i = tid; i < nr; i += FWG) {
+    const int r = r0 + i;
+    if (!root_ok(r)) continue;
+    uint32_t o = cnt[i];
+    const int se = seg_end(r);
+    for (int t = S.fwd[r]; t < se; ++t, ++o) {
       const int h = S.dst[t];
       reinterpret_cast<uint32_t*>(q)[o] = ((uint32_t)r << 16) | (uint32_t)h;
       if (last) {
-        S.flags[r] = 3;
-        S.flags[h] = 3;
+        if (!REWALK) {
+          S.flags[r] = 3;
+          S.flags[h] = 3;
+        }
         reinterpret_cast<uint16_t*>(q + 4 * (int)n2)[o] = 0;
       }
     }
@@ -625,7 +655,7 @@ __device__ __forceinline__ BfsOut<K> bfs_cliques(const FShared& S, FusedHdr& H, 
   __syncthreads();
   out.lvl[2] = 0;
   if constexpr (K > 2) {
-    return BfsLevel<K, 2>::run(S, H, q, qbytes, out, n2, tid);
+    return BfsLevel<K, 2>::template run<REWALK>(S, H, q, qbytes, out, n2, tid, pp);
   } else {
     out.C = n2;
     return out;
@@ -1189,14 +1219,45 @@ void k_fused(FusedArgs A) {
   const int qoff = (L.off_dst + 2 * H.E + 15) & ~15;
   const int qbytes = L.off_parent - qoff;
   char* const q = smem + qoff;
-  const BfsOut<K> bo = bfs_cliques<K>(S, H, q, qbytes, n0, get_cc, (uint32_t)target, tid);
-  const bool bfs_ok = bo.C >= 0;
-  int64_t C;
+  // Root chunks: all roots at once when the levels fit the queue region, else consecutive
+  // root ranges (halved after a level overflows, doubled after a success).  Chunk i covers
+  // roots [rs[i], rs[i+1]) and cliques [cs[i], cs[i+1]) of the micrograph's lexicographic
+  // order; the table lives in cnt behind the n0 entries the level-2 counts use.  A chunk's
+  // tree is rebuilt in P6 (BFS REWALK), except the last one, still in the queue region.
+  uint32_t* const chtab = S.cnt + n0 + 1;
+  // (K = 3 keeps one attempt: the rebuild in P6 would push it past its 64-VGPR budget, and
+  // its level trees rarely overflow)
+  const int maxch = K >= 4 ? min(64, (n + 3 - n0) / 2 - 1) : 1;
+  BfsOut<K> bo;
+  int nch = 0;
+  int64_t C = 0;
+  {
+    int r0 = 0, len = n0;
+    bool ok = maxch >= 1;
+    if (tid == 0) { chtab[0] = 0; chtab[1] = 0; }
+    while (ok && r0 < n0) {
+      len = min(len, n0 - r0);
+      bo = bfs_cliques<K, false>(S, H, q, qbytes, r0, r0 + len, get_cc, (uint32_t)target, tid,
+                                 c.pp);
+      if (bo.C < 0) {
+        ok = K >= 4 && len > 1;
+        len = (len + 1) / 2;
+        continue;
+      }
+      if (nch == maxch) { ok = false; break; }
+      C += bo.C;
+      r0 += len;
+      ++nch;
+      if (tid == 0) { chtab[2 * nch] = (uint32_t)r0; chtab[2 * nch + 1] = (uint32_t)C; }
+      len = 2 * len;
+    }
+    if (!ok) { nch = 0; C = 0; bo.C = -1; }
+  }
+  const bool bfs_ok = nch > 0;
   if (bfs_ok) {
-    C = bo.C;
     // cliques = level-K tree entries (members by walking parents); their flag words follow
-    c.cq_cap = (int)max(C, (int64_t)1);
-    c.cq_ord = reinterpret_cast<uint16_t*>(q + bo.lvl[K] + 4 * (int)C);
+    c.cq_cap = (int)max(bo.C, (int64_t)1);
+    c.cq_ord = reinterpret_cast<uint16_t*>(q + bo.lvl[K] + 4 * (int)bo.C);
   } else {
     S.cbuf = reinterpret_cast<uint16_t*>(smem + qoff);
     c.cq_cap = 0;   // the DFS only counts; P6 re-walks it chunk by chunk
@@ -1303,21 +1364,27 @@ void k_fused(FusedArgs A) {
     const int cap = ufl(c.cq_cap);
     const int64_t obase = (int64_t)(((uint64_t)(uint32_t)ufl((int)(H.base >> 32)) << 32) |
                                     (uint32_t)ufl((int)H.base));
-    // members of chunk slot sl: BFS tree walk, or the re-walk buffer
-    auto clique_members = [&](int sl, int (&mem)[K]) {
-      if (bfs_ok) {
-        BfsLevel<K, K>::prefix(q, bo.lvl, (uint32_t)sl, mem);
-      } else {
-        const uint16_t* sb = S.cbuf + sl * K;
-#pragma unroll
-        for (int i = 0; i < K; ++i) mem[i] = sb[i];
-      }
-    };
-    int ci = 0;
-    for (int c0 = 0; c0 < Cm; c0 += cap, ++ci) {
-      const int c1 = min(Cm, c0 + cap);
+    // BFS: root chunk by chunk (the last one first: its tree is still in the queue region,
+    // the others are rebuilt there); DFS fallback: chunks of <= cap cliques re-walked into cbuf
+    const int nit = bfs_ok ? nch : (Cm + cap - 1) / cap;
+    BfsOut<K> cur = bo;
+    for (int ci = 0; ci < nit; ++ci) {
+      int c0, c1;
       if (tid == 0) H.tief[(ci + 1) & 1] = 0;   // last read before the previous chunk's end
-      if (!bfs_ok) {
+      if (bfs_ok) {
+        const int ch = ci == 0 ? nch - 1 : ci - 1;
+        c0 = ufl((int)chtab[2 * ch + 1]);
+        c1 = ufl((int)chtab[2 * ch + 3]);
+        if constexpr (K >= 4) {
+          if (ci > 0)
+            cur = bfs_cliques<K, true>(S, H, q, qbytes, ufl((int)chtab[2 * ch]),
+                                       ufl((int)chtab[2 * ch + 2]), get_cc, (uint32_t)target,
+                                       tid, c.pp);
+        }
+        c.cq_ord = reinterpret_cast<uint16_t*>(q + cur.lvl[K] + 4 * (c1 - c0));
+      } else {
+        c0 = ci * cap;
+        c1 = min(Cm, c0 + cap);
         c.c0 = c0;
         c.c1 = c1;
         for (int r = tid; r < n0; r += FWG) {
@@ -1330,6 +1397,16 @@ void k_fused(FusedArgs A) {
         }
         __syncthreads();
       }
+      // members of chunk slot sl: BFS tree walk, or the re-walk buffer
+      auto clique_members = [&](int sl, int (&mem)[K]) {
+        if (bfs_ok) {
+          BfsLevel<K, K>::prefix(q, cur.lvl, (uint32_t)sl, mem);
+        } else {
+          const uint16_t* sb = S.cbuf + sl * K;
+#pragma unroll
+          for (int i = 0; i < K; ++i) mem[i] = sb[i];
+        }
+      };
       bool any = false;
       for (int sl = tid; sl < c1 - c0; sl += FWG) {
         int mem[K];
