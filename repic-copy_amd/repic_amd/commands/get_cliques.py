@@ -25,9 +25,14 @@ from .. import _lib
 from ..dist import agree, pair_work, reduce_counts, shard_bounds
 from ..ingest import DirIndex, list_methods, micrograph_names, plan, probe_start_method
 from ..pipeline import Batch, run_batch, split_batches
-from ..writers import Writer, consensus_coords, constraint_matrix, multi_out_coords
+from ..writers import Writer, multi_out_coords
 
 name = "get_cliques"
+
+# phase seconds and totals of the last run in this process (tools/file_bench.py reads them)
+LAST_RUN: dict = {}
+# micrographs per rank from which the writer uses processes instead of threads
+PROC_WRITER_MIN = 512
 
 
 def add_arguments(parser):
@@ -111,6 +116,7 @@ def _shard_weights(in_dir, methods, index, names):
 
 
 def _main(args, ctx, world, rank):
+    t_start = time.time()
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -134,7 +140,12 @@ def _main(args, ctx, world, rank):
     if rank == 0:
         print(f"Using {start} BOX files as starting point")
     names = micrograph_names(index, methods)
+    t_index = time.time() - t_start
     lo, hi = 0, len(names)
+    # large runs write from spawned processes, started now so they import during the parse
+    # and the device work
+    writer = Writer(getattr(args, "threads", None),
+                    processes=len(names) >= PROC_WRITER_MIN * max(1, world))
     if dist is not None:
         b = shard_bounds(_shard_weights(args.in_dir, methods, index, names), world)
         lo, hi = b[rank], b[rank + 1]
@@ -193,11 +204,15 @@ def _main(args, ctx, world, rank):
     else:
         gfail = fail
     share = (t_plan + t_dev) / max(1, len(mgs))
-    writer = Writer(getattr(args, "threads", None))
+    t_write = time.time()
     try:
         _write_all(args, mgs, results, methods, k, lo, fail, gfail, share, writer)
     finally:
         writer.close()
+        LAST_RUN.clear()
+        LAST_RUN.update(index_s=t_index, parse_s=t_plan, device_s=t_dev,
+                        write_s=time.time() - t_write, total_s=time.time() - t_start,
+                        micrographs=len(ok), edges=n_edges, cliques=n_cliques)
         if dist is not None:
             # node-level counters: one reduction at the end of the run
             tot = reduce_counts([len(ok), n_edges, n_cliques])
@@ -229,6 +244,7 @@ def _write_all(args, mgs, results, methods, k, lo, fail, gfail, share, writer):
             raise UnboundLocalError("local variable 'clique' referenced before assignment")
         b0 = int(batch.box_off[j * k])
         idb = int(batch.id_base[j]) - b0
+        cx = cy = cid = coords = None
         if args.multi_out:
             def tup(g):
                 return (float(batch.x[g]), float(batch.y[g]), idb + int(g))
@@ -243,7 +259,6 @@ def _write_all(args, mgs, results, methods, k, lo, fail, gfail, share, writer):
                                       picker_coords)
         else:
             g = r.consensus.astype(np.int64)
-            coords = consensus_coords(batch.x[g], batch.y[g], idb + g)
-        A = constraint_matrix(r.rows, r.n_vert)
-        writer.micrograph(args.out_dir, mg.base, r.w, coords, r.conf, A,
-                          share + (time.time() - t0), r.cc_max, r.cc_cnt)
+            cx, cy, cid = batch.x[g], batch.y[g], idb + g
+        writer.micrograph(args.out_dir, mg.base, r.w, r.conf, r.rows, r.n_vert, cx, cy, cid,
+                          coords, share + (time.time() - t0), r.cc_max, r.cc_cnt)

@@ -68,28 +68,71 @@ def write_micrograph(out_dir, base, w, coords, conf, A, seconds, cc_max, cc_cnt)
         o.write("\t".join([str(seconds), str(cc_max), str(cc_cnt)]) + "\n")
 
 
-class Writer:
-    """Thread-pooled writer: file creation dominates the per-micrograph output cost and
-    releases the GIL, so writes of different micrographs overlap.  ``close()`` waits for
-    every pending write and re-raises the first I/O error."""
+def write_micrograph_raw(out_dir, base, w, conf, rows, n_vert, cx, cy, cid, coords, seconds,
+                         cc_max, cc_cnt):
+    """write_micrograph from the device results: the consensus tuples and the COO matrix are
+    built here (in the writer thread or process), not on the submitting thread."""
+    if coords is None:
+        coords = consensus_coords(cx, cy, cid)
+    write_micrograph(out_dir, base, w, coords, conf, constraint_matrix(rows, n_vert), seconds,
+                     cc_max, cc_cnt)
 
-    def __init__(self, threads=None):
+
+def _write_chunk(items):
+    """Writer-process task: a chunk of (kind, args) writes, in order."""
+    for kind, args in items:
+        if kind == 0:
+            write_skip(*args)
+        else:
+            write_micrograph_raw(*args)
+    return len(items)
+
+
+class Writer:
+    """Pooled writer.  Pickling the per-micrograph objects holds the GIL, so large runs write
+    from a pool of spawned processes (started early, chunks of ``chunk`` micrographs per
+    task, raw arrays shipped, objects built in the worker); small runs use threads (file
+    creation releases the GIL).  ``close()`` waits for every pending write and re-raises the
+    first I/O error, so the files of every micrograph before a crash exist, as in the
+    reference."""
+
+    def __init__(self, threads=None, processes=False, chunk=32):
         self.threads = threads or min(16, (os.cpu_count() or 1))
-        self._pool = ThreadPoolExecutor(max_workers=self.threads) if self.threads > 1 else None
+        self.procs = bool(processes) and self.threads > 1
+        self.chunk = chunk
+        if self.procs:
+            import multiprocessing as mp
+            from concurrent.futures import ProcessPoolExecutor
+            self._pool = ProcessPoolExecutor(self.threads, mp_context=mp.get_context("spawn"))
+            for _ in range(self.threads):   # start the workers now: they import while the
+                self._pool.submit(_write_chunk, [])   # device runs
+        else:
+            self._pool = ThreadPoolExecutor(max_workers=self.threads) if self.threads > 1 else None
         self._futs = []
         self._bases = set()
+        self._items = []
 
-    def _submit(self, fn, *args):
+    def _submit(self, kind, args):
         base = args[1]
         if base in self._bases:      # same output name twice: keep the reference's order
+            self._flush()
             self._drain()
         self._bases.add(base)
         if self._pool is None:
-            fn(*args)
+            _write_chunk([(kind, args)])
+        elif self.procs:
+            self._items.append((kind, args))
+            if len(self._items) >= self.chunk:
+                self._flush()
         else:
-            self._futs.append(self._pool.submit(fn, *args))
-            if len(self._futs) > 4 * self.threads:
-                self._drain(len(self._futs) // 2)
+            self._futs.append(self._pool.submit(_write_chunk, [(kind, args)]))
+        if len(self._futs) > 4 * self.threads:
+            self._drain(len(self._futs) // 2)
+
+    def _flush(self):
+        if self._items:
+            self._futs.append(self._pool.submit(_write_chunk, self._items))
+            self._items = []
 
     def _drain(self, n=None):
         n = len(self._futs) if n is None else n
@@ -98,13 +141,17 @@ class Writer:
             f.result()
 
     def skip(self, out_dir, base):
-        self._submit(write_skip, out_dir, base)
+        self._submit(0, (out_dir, base))
 
-    def micrograph(self, *args):
-        self._submit(write_micrograph, *args)
+    def micrograph(self, out_dir, base, w, conf, rows, n_vert, cx, cy, cid, coords, seconds,
+                   cc_max, cc_cnt):
+        self._submit(1, (out_dir, base, w, conf, rows, n_vert, cx, cy, cid, coords, seconds,
+                         cc_max, cc_cnt))
 
     def close(self):
         try:
+            if self._pool is not None:
+                self._flush()
             self._drain()
         finally:
             if self._pool is not None:

@@ -66,6 +66,16 @@ def test_gpu_multi_batch_split(name, tmp_path):
     _run_case(name, tmp_path, batch_boxes=2000)
 
 
+@pytest.mark.parametrize("name", ["c1_10017", "c1_10017_multi", "skips", "crash_nocliques",
+                                  "ties_getcc"])
+def test_gpu_process_writer_matches_reference_golden(name, tmp_path, monkeypatch):
+    """Large runs write through spawned writer processes (chunks of micrographs): same files,
+    and on a crash the outputs of every micrograph before it exist, as in the reference."""
+    from repic_amd.commands import get_cliques
+    monkeypatch.setattr(get_cliques, "PROC_WRITER_MIN", 1)
+    _run_case(name, tmp_path, threads=4)
+
+
 # ----------------------------------------------------------------------------- vs oracle
 def _oracle_mg(mg, box, methods, id_base, get_cc=False):
     from oracle import cpu_ref
