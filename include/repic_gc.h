@@ -122,6 +122,23 @@ int rgc_kernel_times(rgc_ctx* ctx, int max_n, float* ms, const char** names);
  * valid until the next rgc_run; returns the edge count (order unspecified). */
 int64_t rgc_last_edges(rgc_ctx* ctx, const int32_t** u, const int32_t** v, const double** ji);
 
+/* score_detections (repic/utils/score_detections.py:16-48 get_segmentation_scores): for every
+ * (ground truth, picker) pair, the pixel counts of the int16 masks the reference paints.
+ * Boxes are given as numpy slice bounds already normalised on the host (row start < row end
+ * <= height, col start < col end <= width; boxes with an empty slice are left out), picked
+ * boxes already filtered by the confidence threshold.  counts[3p..3p+2] = sum(gt_arr),
+ * sum(pckr_arr), sum(gt_arr * pckr_arr).  RGC_F_TIMING records "k_score_raster". */
+typedef struct rgc_score_in {
+  int64_t n_pairs;
+  const int64_t* height;   /* [n_pairs] mask rows (mrc_h) */
+  const int64_t* width;    /* [n_pairs] mask columns (mrc_w) */
+  const int64_t* gt_off;   /* [n_pairs + 1] pair p's ground truth: boxes[gt_off[p], gt_off[p+1]) */
+  const int64_t* pk_off;   /* [n_pairs + 1] pair p's picks: boxes[pk_off[p], pk_off[p+1]) */
+  const int32_t* boxes;    /* [n_boxes][4] row start, row end, col start, col end */
+  uint32_t flags;          /* RGC_F_TIMING */
+} rgc_score_in;
+int rgc_score_pairs(rgc_ctx* ctx, const rgc_score_in* in, int64_t* counts);
+
 int rgc_parse_files(const char* const* paths, int64_t n_files, int n_threads, rgc_parsed** out);
 void rgc_parsed_free(rgc_parsed* p);
 

@@ -62,6 +62,8 @@ enum DevBufId {
   D_LCNT, D_LOFF, D_LROOT0, D_LROOT1, D_LM0, D_LM1, D_LP0, D_LP1,
   // RGC_F_EDGES test hook
   D_EU, D_EV, D_EJIOUT,
+  // score_detections raster
+  D_SC_BOX, D_SC_GOFF, D_SC_POFF, D_SC_TP, D_SC_TR, D_SC_TW, D_SC_CNT,
   D_COUNT
 };
 enum HostBufId {
@@ -966,6 +968,98 @@ int64_t rgc_last_edges(rgc_ctx* c, const int32_t** u, const int32_t** v, const d
   if (v) *v = H<int32_t>(c, H_EV);
   if (ji) *ji = H<double>(c, H_EJIOUT);
   return c->n_edge_dump;
+}
+
+int rgc_score_pairs(rgc_ctx* c, const rgc_score_in* in, int64_t* counts) {
+  if (!c || !in || !counts) return fail("null argument");
+  HIPCHK(hipSetDevice(c->device));
+  const int64_t np = in->n_pairs;
+  if (np < 0 || np > INT32_MAX) return fail("n_pairs out of range");
+  c->times.clear();
+  c->time_names.clear();
+  if (np == 0) return 0;
+  const int64_t nb = std::max(in->pk_off[np], in->gt_off[np]);   // boxes in the array
+  if (in->gt_off[0] < 0 || in->pk_off[0] < 0) return fail("negative box offset");
+  // tiles: R rows x TW words, R * TW = the kernel's LDS words per mask
+  const int words_cap = rgc::score_tile_words();
+  std::vector<int> tp, tr, tw;
+  int R = 0, TW = 0;
+  int64_t maxw = 1;
+  for (int64_t p = 0; p < np; ++p) maxw = std::max<int64_t>(maxw, (in->width[p] + 63) / 64);
+  TW = (int)std::min<int64_t>(maxw, 32);
+  R = words_cap / TW;
+  for (int64_t p = 0; p < np; ++p) {
+    const int64_t H = in->height[p], W = in->width[p];
+    if (H < 0 || W < 0 || H > (1 << 30) || W > (1 << 30)) return fail("mask size out of range");
+    if (in->gt_off[p + 1] < in->gt_off[p] || in->pk_off[p + 1] < in->pk_off[p] ||
+        in->pk_off[p + 1] > nb)
+      return fail("box offsets must be non-decreasing and within the box array");
+    for (int which = 0; which < 2; ++which) {
+      const int64_t* off = which ? in->pk_off : in->gt_off;
+      for (int64_t b = off[p]; b < off[p + 1]; ++b) {
+        const int32_t* q = in->boxes + 4 * b;
+        if (!(0 <= q[0] && q[0] < q[1] && q[1] <= H && 0 <= q[2] && q[2] < q[3] && q[3] <= W))
+          return fail("box " + std::to_string(b) + " is not a normalised non-empty slice");
+      }
+    }
+    const int64_t nw = (W + 63) / 64;
+    for (int64_t r0 = 0; r0 < H; r0 += R)
+      for (int64_t w0 = 0; w0 < nw; w0 += TW) {
+        tp.push_back((int)p);
+        tr.push_back((int)r0);
+        tw.push_back((int)w0);
+      }
+  }
+  const int64_t nt = (int64_t)tp.size();
+  if (nt > INT32_MAX) return fail("too many tiles");
+  TRY(ensure_dev(c, D_SC_BOX, (size_t)nb * 16));
+  TRY(ensure_dev(c, D_SC_GOFF, (size_t)(np + 1) * 8));
+  TRY(ensure_dev(c, D_SC_POFF, (size_t)(np + 1) * 8));
+  TRY(ensure_dev(c, D_SC_TP, (size_t)nt * 4));
+  TRY(ensure_dev(c, D_SC_TR, (size_t)nt * 4));
+  TRY(ensure_dev(c, D_SC_TW, (size_t)nt * 4));
+  TRY(ensure_dev(c, D_SC_CNT, (size_t)np * 24));
+  hipStream_t s = c->stream;
+  if (nb) HIPCHK(hipMemcpyAsync(c->d[D_SC_BOX].p, in->boxes, (size_t)nb * 16, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(c->d[D_SC_GOFF].p, in->gt_off, (size_t)(np + 1) * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(c->d[D_SC_POFF].p, in->pk_off, (size_t)(np + 1) * 8, hipMemcpyHostToDevice, s));
+  if (nt) {
+    HIPCHK(hipMemcpyAsync(c->d[D_SC_TP].p, tp.data(), (size_t)nt * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->d[D_SC_TR].p, tr.data(), (size_t)nt * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->d[D_SC_TW].p, tw.data(), (size_t)nt * 4, hipMemcpyHostToDevice, s));
+  }
+  HIPCHK(hipMemsetAsync(c->d[D_SC_CNT].p, 0, (size_t)np * 24, s));
+  rgc::ScoreArgs A;
+  A.boxes = D<int4>(c, D_SC_BOX);
+  A.gt_off = D<int64_t>(c, D_SC_GOFF);
+  A.pk_off = D<int64_t>(c, D_SC_POFF);
+  A.tile_pair = D<int>(c, D_SC_TP);
+  A.tile_r0 = D<int>(c, D_SC_TR);
+  A.tile_w0 = D<int>(c, D_SC_TW);
+  A.R = R;
+  A.TW = TW;
+  A.counts = D<unsigned long long>(c, D_SC_CNT);
+  const bool timing = (in->flags & RGC_F_TIMING) != 0;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (timing) {
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, s));
+  }
+  rgc::launch_score_raster(s, (int)nt, A);
+  HIPCHK(hipGetLastError());
+  if (timing) HIPCHK(hipEventRecord(e1, s));
+  HIPCHK(hipMemcpyAsync(counts, c->d[D_SC_CNT].p, (size_t)np * 24, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (timing) {
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    c->times.push_back(ms);
+    c->time_names.push_back("k_score_raster");
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+  }
+  return 0;
 }
 
 uint64_t rgc_py_hash_node(double x, double y, int64_t id) { return pyset::hash_node(x, y, id); }

@@ -190,4 +190,18 @@ void launch_rank(hipStream_t stream, int N, int n_mg, int k, const int32_t* box_
                  const int32_t* bmg, const MgGrid* grid, const double* x, const double* y,
                  const uint8_t* in_clique, int32_t* bcnt, int32_t* bslot, int64_t* boff,
                  int64_t* tile_buf, int64_t* total, int32_t* vsort, int32_t* vrow, MgStat* st);
+// score_detections raster/reduce (rgc_score.hip): one workgroup per (pair, tile)
+struct ScoreArgs {
+  const int4* boxes;          // (row start, row end, col start, col end), numpy slice bounds
+  const int64_t* gt_off;      // [n_pairs + 1]
+  const int64_t* pk_off;      // [n_pairs + 1]
+  const int* tile_pair;       // per tile: pair, first row, first 64-pixel word
+  const int* tile_r0;
+  const int* tile_w0;
+  int R, TW;                  // tile = R rows x TW words (R * TW <= score_tile_words())
+  unsigned long long* counts; // [n_pairs][3] = sum(gt), sum(pckr), sum(gt * pckr)
+};
+int score_tile_words();
+void launch_score_raster(hipStream_t stream, int n_tiles, const ScoreArgs& A);
+
 }  // namespace rgc
