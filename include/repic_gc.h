@@ -139,6 +139,23 @@ typedef struct rgc_score_in {
 } rgc_score_in;
 int rgc_score_pairs(rgc_ctx* ctx, const rgc_score_in* in, int64_t* counts);
 
+/* run_ilp (repic/commands/run_ilp.py:50-63): maximise w.x over binary x subject to A x <= 1,
+ * exactly, for a batch of micrographs at once (rows are global box ids: micrographs never
+ * share a row).  A is given in CSC form.  x[c] = 1 for the chosen columns (cliques);
+ * exact[c] = 1 when column c's conflict component was solved to proven optimality (0: the
+ * component hit node_limit and x holds the best packing found).  RGC_F_TIMING records the
+ * stages in rgc_kernel_times. */
+typedef struct rgc_ilp_in {
+  int64_t n_cols;          /* cliques */
+  int64_t n_rows;          /* boxes */
+  const int64_t* col_ptr;  /* [n_cols + 1] column c's rows: row_idx[col_ptr[c], col_ptr[c+1]) */
+  const int32_t* row_idx;  /* [nnz] global row ids */
+  const double* w;         /* [n_cols] objective */
+  int64_t node_limit;      /* branch-and-bound nodes per component (0: 2^22) */
+  uint32_t flags;          /* RGC_F_TIMING */
+} rgc_ilp_in;
+int rgc_ilp_solve(rgc_ctx* ctx, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact);
+
 int rgc_parse_files(const char* const* paths, int64_t n_files, int n_threads, rgc_parsed** out);
 void rgc_parsed_free(rgc_parsed* p);
 

@@ -64,6 +64,10 @@ enum DevBufId {
   D_EU, D_EV, D_EJIOUT,
   // score_detections raster
   D_SC_BOX, D_SC_GOFF, D_SC_POFF, D_SC_TP, D_SC_TR, D_SC_TW, D_SC_CNT,
+  // run_ilp set packing
+  D_IL_CPTR, D_IL_ROW, D_IL_W, D_IL_REP, D_IL_PAR, D_IL_ROOT, D_IL_CSIZE, D_IL_RCNT, D_IL_RCUR,
+  D_IL_RPTR, D_IL_RCOLS, D_IL_CID, D_IL_CN, D_IL_COFF, D_IL_CCUR, D_IL_MEM, D_IL_LOC, D_IL_SCR,
+  D_IL_BIG, D_IL_NBIG, D_IL_WSCR, D_IL_X, D_IL_EX, D_IL_RLOC,
   D_COUNT
 };
 enum HostBufId {
@@ -1058,6 +1062,140 @@ int rgc_score_pairs(rgc_ctx* c, const rgc_score_in* in, int64_t* counts) {
     c->time_names.push_back("k_score_raster");
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
+  }
+  return 0;
+}
+
+int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) {
+  if (!c || !in || !x || !exact) return fail("null argument");
+  HIPCHK(hipSetDevice(c->device));
+  const int64_t nc = in->n_cols, nr = in->n_rows;
+  if (nc < 0 || nc >= INT32_MAX || nr < 0 || nr >= INT32_MAX) return fail("n_cols / n_rows out of range");
+  c->times.clear();
+  c->time_names.clear();
+  c->n_ev = 0;
+  c->timing = (in->flags & RGC_F_TIMING) != 0;
+  if (nc == 0) return 0;
+  const int64_t nnz = in->col_ptr[nc];
+  if (in->col_ptr[0] != 0 || nnz < 0) return fail("col_ptr must start at 0");
+  int kmax = 1;
+  for (int64_t j = 0; j < nc; ++j) {
+    const int64_t d = in->col_ptr[j + 1] - in->col_ptr[j];
+    if (d < 1) return fail("every column needs at least one row");
+    kmax = (int)std::max<int64_t>(kmax, d);
+  }
+  if (kmax > 8) return fail("columns of more than 8 rows (cliques of more than 8 boxes)");
+  for (int64_t e = 0; e < nnz; ++e)
+    if (in->row_idx[e] < 0 || in->row_idx[e] >= nr) return fail("row index out of range");
+  hipStream_t s = c->stream;
+  TRY(ensure_dev(c, D_IL_CPTR, (nc + 1) * 8));
+  TRY(ensure_dev(c, D_IL_ROW, nnz * 4));
+  TRY(ensure_dev(c, D_IL_W, nc * 8));
+  TRY(ensure_dev(c, D_IL_REP, nr * 4));
+  TRY(ensure_dev(c, D_IL_PAR, nc * 4));
+  TRY(ensure_dev(c, D_IL_ROOT, nc * 4));
+  TRY(ensure_dev(c, D_IL_CSIZE, nc * 4));
+  TRY(ensure_dev(c, D_IL_RCNT, nr * 4));
+  TRY(ensure_dev(c, D_IL_RCUR, nr * 4));
+  TRY(ensure_dev(c, D_IL_RPTR, (nr + 1) * 8));
+  TRY(ensure_dev(c, D_IL_RCOLS, nnz * 4));
+  TRY(ensure_dev(c, D_IL_CID, (nc + 1) * 8));
+  TRY(ensure_dev(c, D_IL_MEM, nc * 4));
+  TRY(ensure_dev(c, D_IL_LOC, nc * 4));
+  TRY(ensure_dev(c, D_IL_SCR, (size_t)nc * (2 * kmax + 8) * 8));
+  TRY(ensure_dev(c, D_IL_RLOC, nr * 4));
+  TRY(ensure_dev(c, D_IL_NBIG, 16));
+  TRY(ensure_dev(c, D_IL_X, nc));
+  TRY(ensure_dev(c, D_IL_EX, nc));
+  TRY(ensure_dev(c, D_TILES, scan_tiles_needed(std::max(nc, nr) + 1) * 8));
+  TRY(ensure_dev(c, D_TOTAL, 32));
+  TRY(ensure_host(c, H_TOTAL, 64));
+  HIPCHK(hipMemcpyAsync(c->d[D_IL_CPTR].p, in->col_ptr, (nc + 1) * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(c->d[D_IL_ROW].p, in->row_idx, nnz * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(c->d[D_IL_W].p, in->w, nc * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(c->d[D_IL_NBIG].p, 0, 16, s));
+  rgc::IlpArgs A{};
+  A.n_cols = nc;
+  A.n_rows = nr;
+  A.kmax = kmax;
+  A.node_limit = in->node_limit > 0 ? in->node_limit : (int64_t)1 << 22;
+  A.col_ptr = D<int64_t>(c, D_IL_CPTR);
+  A.row_idx = D<int32_t>(c, D_IL_ROW);
+  A.w = D<double>(c, D_IL_W);
+  A.rep = D<int32_t>(c, D_IL_REP);
+  A.rloc = D<int32_t>(c, D_IL_RLOC);
+  A.parent = D<int32_t>(c, D_IL_PAR);
+  A.is_root = D<int32_t>(c, D_IL_ROOT);
+  A.csize = D<int32_t>(c, D_IL_CSIZE);
+  A.rcnt = D<int32_t>(c, D_IL_RCNT);
+  A.rcur = D<int32_t>(c, D_IL_RCUR);
+  A.rptr = D<int64_t>(c, D_IL_RPTR);
+  A.rcols = D<int32_t>(c, D_IL_RCOLS);
+  A.comp_id = D<int64_t>(c, D_IL_CID);
+  A.members = D<int32_t>(c, D_IL_MEM);
+  A.loc = D<int32_t>(c, D_IL_LOC);
+  A.scratch = D<uint64_t>(c, D_IL_SCR);
+  A.n_big = D<unsigned int>(c, D_IL_NBIG);
+  A.x = D<uint8_t>(c, D_IL_X);
+  A.exact = D<uint8_t>(c, D_IL_EX);
+  TRY(mark(c, "k_ilp_components"));
+  rgc::launch_ilp(s, 0, A, 0, 0);
+  launch_scan(s, nc, A.is_root, D<int64_t>(c, D_IL_CID), D<int64_t>(c, D_TILES),
+              D<int64_t>(c, D_TOTAL));
+  HIPCHK(hipMemcpyAsync(H<int64_t>(c, H_TOTAL), D<int64_t>(c, D_TOTAL), 8, hipMemcpyDeviceToHost, s));
+  launch_scan(s, nr, A.rcnt, D<int64_t>(c, D_IL_RPTR), D<int64_t>(c, D_TILES),
+              D<int64_t>(c, D_TOTAL) + 1);
+  HIPCHK(hipStreamSynchronize(s));
+  const int64_t ncomp = H<int64_t>(c, H_TOTAL)[0];
+  TRY(ensure_dev(c, D_IL_CN, (ncomp + 1) * 4));
+  TRY(ensure_dev(c, D_IL_COFF, (ncomp + 1) * 8));
+  TRY(ensure_dev(c, D_IL_CCUR, (ncomp + 1) * 4));
+  TRY(ensure_dev(c, D_IL_BIG, (ncomp + 1) * 4));
+  A.n_comp = ncomp;
+  A.comp_n = D<int32_t>(c, D_IL_CN);
+  A.comp_off = D<int64_t>(c, D_IL_COFF);
+  A.comp_cur = D<int32_t>(c, D_IL_CCUR);
+  A.big = D<int32_t>(c, D_IL_BIG);
+  rgc::launch_ilp(s, 1, A, 0, 0);
+  launch_scan(s, ncomp, A.comp_n, D<int64_t>(c, D_IL_COFF), D<int64_t>(c, D_TILES),
+              D<int64_t>(c, D_TOTAL) + 2);
+  HIPCHK(hipMemsetAsync(A.comp_cur, 0, (ncomp + 1) * 4, s));
+  rgc::launch_ilp(s, 2, A, 0, 0);
+  TRY(mark(c, "k_ilp_small"));
+  rgc::launch_ilp(s, 3, A, 0, 0);
+  HIPCHK(hipMemcpyAsync(H<int64_t>(c, H_TOTAL) + 1, A.n_big, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const int n_big = (int)*reinterpret_cast<uint32_t*>(H<int64_t>(c, H_TOTAL) + 1);
+  if (n_big > 0) {
+    std::vector<int32_t> big(n_big), cn(ncomp);
+    HIPCHK(hipMemcpyAsync(big.data(), A.big, n_big * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(cn.data(), A.comp_n, ncomp * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    int nmax = 0;
+    for (int b : big) nmax = std::max(nmax, std::min(cn[b], rgc::ilp_big_max()));
+    const int64_t W = (nmax + 63) / 64;
+    // adjacency n W, stack n (W + 2), weights n, tmpid K n / 2, row info (K + 1) n / 4
+    A.wstride = (int64_t)nmax * W + (int64_t)nmax * (W + 2) + nmax +
+                ((int64_t)kmax * nmax + 1) / 2 + ((int64_t)(kmax + 1) * nmax + 3) / 4 + 8;
+    const int n_waves = std::min(n_big, 2048);
+    TRY(ensure_dev(c, D_IL_WSCR, (size_t)n_waves * A.wstride * 8));
+    A.wscratch = D<uint64_t>(c, D_IL_WSCR);
+    TRY(mark(c, "k_ilp_wave"));
+    rgc::launch_ilp(s, 4, A, n_big, n_waves);
+  }
+  TRY(mark(c, "d2h_x"));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(x, A.x, nc, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(exact, A.exact, nc, hipMemcpyDeviceToHost, s));
+  TRY(mark(c, "end"));
+  HIPCHK(hipStreamSynchronize(s));
+  if (c->timing) {
+    for (int i = 0; i + 1 < c->n_ev; ++i) {
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, c->events[i], c->events[i + 1]));
+      c->times.push_back(ms);
+      c->time_names.push_back(c->ev_names[i]);
+    }
   }
   return 0;
 }

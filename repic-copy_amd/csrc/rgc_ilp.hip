@@ -1,0 +1,504 @@
+// rgc_ilp.hip — exact max-weight set packing: the ILP of run_ilp.
+//
+// Reference repic/commands/run_ilp.py:50-63: per micrograph, binary x over the cliques
+// (columns of the constraint matrix A), maximise w.x subject to A x <= 1 (every box in at most
+// one chosen clique), solved there by Gurobi.  Two cliques conflict iff they share a box, and
+// the problem splits into the connected components of that conflict graph (cliques of a box
+// graph component, usually a handful).  Pipeline (all on the device, one batch of many
+// micrographs; rows are global box ids, so micrographs never mix):
+//   1. k_ilp_rep / k_ilp_union / k_ilp_root: lock-free union-find of the columns through
+//      their rows (each row links its columns to the smallest one).
+//   2. components numbered by a scan over roots, member lists filled, rows -> columns CSR.
+//   3. k_ilp_small: one THREAD per component of 2..64 cliques; k_ilp_wave: one WAVEFRONT per
+//      larger component (bitsets one 64-bit word per lane, up to 4096 cliques).  Both run the
+//      same depth-first branch and bound over candidates sorted by weight (include the
+//      heaviest remaining candidate first, then exclude it), pruning with the box-partition
+//      bound: assign every candidate to one of its boxes (its a-th row); at most one
+//      candidate per box can be chosen, so sum over boxes of the heaviest candidate is an
+//      upper bound; the minimum over the k assignments is used.  Weights are f32 values
+//      summed in f64 (exact), so "optimal" is exact.  A component that exceeds the node
+//      limit keeps the best packing found and is reported as not proven optimal.
+#include "rgc_kernels.h"
+
+#include <climits>
+
+namespace rgc {
+
+constexpr int ILP_WG = 256;
+constexpr int ILP_SMALL = 64;     // thread-per-component limit (one 64-bit mask)
+constexpr int ILP_BIG = 4096;     // wave-per-component limit (64 lanes x 64 bits)
+
+__device__ __forceinline__ int32_t ilp_find(int32_t* p, int32_t x) {
+  for (;;) {
+    const int32_t q = __hip_atomic_load(p + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (q == x) return x;
+    const int32_t g = __hip_atomic_load(p + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (g != q) __hip_atomic_store(p + x, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    x = g;
+  }
+}
+
+__device__ __forceinline__ void ilp_union(int32_t* p, int32_t a, int32_t b) {
+  for (;;) {
+    a = ilp_find(p, a);
+    b = ilp_find(p, b);
+    if (a == b) return;
+    if (a < b) { const int32_t t = a; a = b; b = t; }
+    if (atomicCAS(p + a, a, b) == a) return;
+  }
+}
+
+__global__ __launch_bounds__(ILP_WG) void k_ilp_init(IlpArgs A) {
+  const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (c < A.n_cols) {
+    A.parent[c] = (int32_t)c;
+    A.csize[c] = 0;
+  }
+  if (c < A.n_rows) {
+    A.rep[c] = INT_MAX;
+    A.rloc[c] = INT_MAX;
+    A.rcnt[c] = 0;
+    A.rcur[c] = 0;
+  }
+}
+
+// 1. smallest column of every row
+__global__ __launch_bounds__(ILP_WG) void k_ilp_rep(IlpArgs A) {
+  const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (c >= A.n_cols) return;
+  for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e) atomicMin(A.rep + A.row_idx[e], (int)c);
+}
+
+__global__ __launch_bounds__(ILP_WG) void k_ilp_union(IlpArgs A) {
+  const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (c >= A.n_cols) return;
+  for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e) {
+    const int32_t r = A.rep[A.row_idx[e]];
+    if (r != (int32_t)c) ilp_union(A.parent, (int32_t)c, r);
+  }
+}
+
+// compress; root flags (for the component scan) and component sizes by root; rows -> column
+// counts (the transpose's CSR)
+__global__ __launch_bounds__(ILP_WG) void k_ilp_root(IlpArgs A) {
+  const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (c >= A.n_cols) return;
+  const int32_t r = ilp_find(A.parent, (int32_t)c);
+  A.parent[c] = r;
+  A.is_root[c] = r == (int32_t)c ? 1 : 0;
+  atomicAdd(A.csize + r, 1);
+  for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e) atomicAdd(A.rcnt + A.row_idx[e], 1);
+}
+
+// component sizes in component order (comp id = scanned root index)
+__global__ __launch_bounds__(ILP_WG) void k_ilp_csize(IlpArgs A) {
+  const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (c >= A.n_cols || !A.is_root[c]) return;
+  A.comp_n[A.comp_id[c]] = A.csize[c];
+}
+
+// member lists (arbitrary order; the solvers sort them) and the rows -> columns lists
+__global__ __launch_bounds__(ILP_WG) void k_ilp_fill(IlpArgs A) {
+  const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (c >= A.n_cols) return;
+  const int64_t comp = A.comp_id[A.parent[c]];
+  const int slot = atomicAdd(A.comp_cur + comp, 1);
+  A.members[A.comp_off[comp] + slot] = (int32_t)c;
+  for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e) {
+    const int32_t r = A.row_idx[e];
+    A.rcols[A.rptr[r] + atomicAdd(A.rcur + r, 1)] = (int32_t)c;
+  }
+}
+
+// Local numbering of a component: members sorted by (weight desc, column asc), so the lowest
+// set bit of a candidate set is its heaviest candidate.  Rank sort: member i's position is
+// the number of members that come before it (lanes / threads share the O(n^2) count).
+__device__ __forceinline__ bool ilp_before(const IlpArgs& A, int32_t d, int32_t c) {
+  const double wd = A.w[d], wc = A.w[c];
+  return wd > wc || (wd == wc && d < c);
+}
+
+// Local rows (boxes) of a component and each member's packed row info, in scratch:
+// lr[i * (K + 1) + a] = local id of member i's a-th row (a < deg; padded with its last row),
+// lr[i * (K + 1) + K] = its opener box: the row with the most columns (ties: first).  Local
+// ids via the winner of an atomicMin over member slots (i * K + a) on the global row array
+// rloc (rows belong to one component only), then a counter.  Steps are separated by the
+// caller's barriers: step 0 claims, step 1 numbers the winners, step 2 writes lr.
+template <bool SERIAL>
+__device__ void ilp_rows_step(const IlpArgs& A, const int32_t* m, int n, int K, int step, int i0,
+                              int di, int32_t* tmpid, uint16_t* lr, int* counter) {
+  for (int i = i0; i < n; i += di) {
+    const int32_t c = m[i];
+    const int64_t e0 = A.col_ptr[c], e1 = A.col_ptr[c + 1];
+    int best_deg = -1, best_row = 0;
+    for (int a = 0; a < K; ++a) {
+      const int64_t e = e0 + a < e1 ? e0 + a : e1 - 1;
+      const int32_t r = A.row_idx[e];
+      const int32_t slot = i * K + a;
+      if (step == 0) {
+        if (e0 + a < e1) atomicMin(A.rloc + r, slot);
+      } else if (step == 1) {
+        if (e0 + a < e1 && A.rloc[r] == slot) tmpid[slot] = SERIAL ? (*counter)++ : atomicAdd(counter, 1);
+      } else {
+        const int id = tmpid[A.rloc[r]];
+        lr[i * (K + 1) + a] = (uint16_t)id;
+        const int deg = (int)(A.rptr[r + 1] - A.rptr[r]);
+        if (deg > best_deg) { best_deg = deg; best_row = id; }
+      }
+    }
+    if (step == 2) lr[i * (K + 1) + K] = (uint16_t)best_row;
+  }
+}
+
+// One thread per component of 2..64 cliques.  Scratch ((2 kmax + 8) 64-bit words per member
+// at the component's offset): weights, adjacency masks, DFS stack, row info.  The bound is a
+// greedy clique cover of the candidates by boxes: heaviest first, a candidate with one of its
+// boxes already opened joins that box's group (it conflicts with every member), otherwise it
+// opens its opener box and adds its weight.  At most one candidate per group can be chosen,
+// so the sum of the openers' weights bounds the best packing of the candidates.
+constexpr int ILP_SMALL_ROWWORDS = ILP_SMALL * 8 / 64;   // open-box bits per thread (K <= 8)
+
+__global__ __launch_bounds__(ILP_WG) void k_ilp_small(IlpArgs A) {
+  __shared__ uint64_t open_lds[ILP_WG][ILP_SMALL_ROWWORDS];
+  const int64_t comp = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (comp >= A.n_comp) return;
+  const int n = A.comp_n[comp];
+  const int64_t off = A.comp_off[comp];
+  int32_t* m = A.members + off;
+  if (n == 1) {
+    const int32_t c = m[0];
+    A.x[c] = A.w[c] > 0.0 ? 1 : 0;
+    A.exact[c] = 1;
+    return;
+  }
+  if (n > ILP_SMALL) return;
+  const int K = A.kmax;
+  double* wl = reinterpret_cast<double*>(A.scratch + off * (2 * K + 8));   // n
+  uint64_t* adj = reinterpret_cast<uint64_t*>(wl + n);                    // n
+  uint64_t* stk = adj + n;                                                 // 3 n
+  int32_t* tmpid = reinterpret_cast<int32_t*>(stk + 3 * n);                // K n
+  uint16_t* lr = reinterpret_cast<uint16_t*>(tmpid + K * n);               // (K + 1) n
+  int32_t* sorted = reinterpret_cast<int32_t*>(stk);                       // (before the DFS)
+  // rank sort by (weight desc, column asc)
+  for (int i = 0; i < n; ++i) {
+    int r = 0;
+    for (int q = 0; q < n; ++q) r += ilp_before(A, m[q], m[i]) ? 1 : 0;
+    sorted[r] = m[i];
+  }
+  for (int i = 0; i < n; ++i) m[i] = sorted[i];
+  for (int i = 0; i < n; ++i) {
+    A.loc[m[i]] = i;
+    wl[i] = A.w[m[i]];
+  }
+  int nrow = 0;
+  for (int step = 0; step < 3; ++step) ilp_rows_step<true>(A, m, n, K, step, 0, 1, tmpid, lr, &nrow);
+  for (int i = 0; i < n; ++i) {
+    uint64_t a = 0;
+    const int32_t c = m[i];
+    for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e) {
+      const int32_t r = A.row_idx[e];
+      for (int64_t f = A.rptr[r]; f < A.rptr[r + 1]; ++f) a |= 1ull << A.loc[A.rcols[f]];
+    }
+    adj[i] = a & ~(1ull << i);
+  }
+  uint64_t* open = open_lds[threadIdx.x];
+  const int ow = (nrow + 63) / 64;
+  auto bound = [&](uint64_t P) {
+    for (int q = 0; q < ow; ++q) open[q] = 0;
+    double s = 0.0;
+    while (P) {
+      const int i = __builtin_ctzll(P);
+      P &= P - 1;
+      const uint16_t* li = lr + i * (K + 1);
+      bool cov = false;
+      for (int a = 0; a < K; ++a) cov |= (open[li[a] >> 6] >> (li[a] & 63)) & 1;
+      if (!cov) {
+        open[li[K] >> 6] |= 1ull << (li[K] & 63);
+        s += wl[i];
+      }
+    }
+    return s;
+  };
+  const uint64_t all = (n == 64) ? ~0ull : ((1ull << n) - 1);
+  double best = -1.0, cur = 0.0;
+  uint64_t best_set = 0, chosen = 0, P = all;
+  int depth = 0;
+  int64_t nodes = 0;
+  bool exact = true;
+  for (;;) {
+    bool back = false;
+    if (++nodes > A.node_limit) { exact = false; break; }
+    if (P == 0) {
+      if (cur > best) { best = cur; best_set = chosen; }
+      back = true;
+    } else if (cur + bound(P) <= best) {
+      back = true;
+    } else {
+      // include the heaviest candidate j (lowest bit) first; its frame keeps P and cur
+      const int j = __builtin_ctzll(P);
+      stk[3 * depth] = P;
+      stk[3 * depth + 1] = (uint64_t)__double_as_longlong(cur);
+      stk[3 * depth + 2] = ((uint64_t)j << 1) | 1u;
+      ++depth;
+      P &= ~adj[j] & ~(1ull << j);
+      cur += wl[j];
+      chosen |= 1ull << j;
+    }
+    if (back) {
+      // unwind to the nearest frame still on its include branch and take its exclude branch
+      bool found = false;
+      while (depth > 0) {
+        const uint64_t fr = stk[3 * (depth - 1) + 2];
+        const int j = (int)(fr >> 1);
+        if (fr & 1u) {
+          stk[3 * (depth - 1) + 2] = (uint64_t)j << 1;
+          P = stk[3 * (depth - 1)] & ~(1ull << j);
+          cur = __longlong_as_double((long long)stk[3 * (depth - 1) + 1]);
+          chosen &= (1ull << j) - 1;   // earlier frames chose only members < j
+          found = true;
+          break;
+        }
+        --depth;
+      }
+      if (!found) break;
+    }
+  }
+  for (int i = 0; i < n; ++i) {
+    A.x[m[i]] = (best_set >> i) & 1 ? 1 : 0;
+    A.exact[m[i]] = exact ? 1 : 0;
+  }
+}
+
+// list of the components handled by the wave solver
+__global__ __launch_bounds__(ILP_WG) void k_ilp_biglist(IlpArgs A) {
+  const int64_t comp = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (comp >= A.n_comp) return;
+  if (A.comp_n[comp] > ILP_SMALL) A.big[atomicAdd(A.n_big, 1u)] = (int32_t)comp;
+}
+
+constexpr int ILP_LRCAP = 16384;   // u16 row-info entries kept in LDS (wave solver)
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+// One wavefront per component of 65..4096 cliques (persistent: waves take components from
+// the list).  Lane l holds word l of every bitset; adjacency rows and the DFS stack in the
+// wave's scratch; open boxes and (when they fit) the members' row info in LDS.  The greedy
+// clique-cover bound runs 64 candidates at a time: candidates covered by boxes opened in
+// earlier chunks drop out, then the lowest (heaviest) uncovered lane opens its box and the
+// lanes holding that box drop out, until none is left - the sequential greedy's result.
+__global__ __launch_bounds__(64) void k_ilp_wave(IlpArgs A, int n_big) {
+  __shared__ uint64_t open[ILP_BIG * 8 / 64];
+  __shared__ uint16_t lrs[ILP_LRCAP];
+  __shared__ int counter;
+  const int lane = threadIdx.x;
+  uint64_t* base = A.wscratch + (int64_t)blockIdx.x * A.wstride;
+  for (int bi = blockIdx.x; bi < n_big; bi += gridDim.x) {
+    const int64_t comp = A.big[bi];
+    const int n = A.comp_n[comp];
+    int32_t* m = A.members + A.comp_off[comp];
+    if (n > ILP_BIG) {
+      for (int i = lane; i < n; i += 64) { A.x[m[i]] = 0; A.exact[m[i]] = 0; }
+      continue;
+    }
+    const int W = (n + 63) / 64;
+    const int K = A.kmax;
+    uint64_t* adj = base;                                         // n W
+    uint64_t* stk = adj + (int64_t)n * W;                         // n (W + 2)
+    double* wl = reinterpret_cast<double*>(stk + (int64_t)n * (W + 2));   // n
+    int32_t* tmpid = reinterpret_cast<int32_t*>(wl + n);          // K n
+    uint16_t* lrg = reinterpret_cast<uint16_t*>(tmpid + (int64_t)K * n);   // (K + 1) n
+    int32_t* sorted = reinterpret_cast<int32_t*>(stk);
+    for (int i = lane; i < n; i += 64) {
+      int r = 0;
+      for (int q = 0; q < n; ++q) r += ilp_before(A, m[q], m[i]) ? 1 : 0;
+      sorted[r] = m[i];
+    }
+    wave_sync();
+    for (int i = lane; i < n; i += 64) {
+      m[i] = sorted[i];
+      A.loc[sorted[i]] = i;
+      wl[i] = A.w[sorted[i]];
+    }
+    if (lane == 0) counter = 0;
+    wave_sync();
+    for (int step = 0; step < 3; ++step) {
+      ilp_rows_step<false>(A, m, n, K, step, lane, 64, tmpid, lrg, &counter);
+      wave_sync();
+    }
+    const int nrow = counter;
+    // adjacency rows: lane i builds row i's words
+    for (int i = lane; i < n; i += 64) {
+      uint64_t* row = adj + (int64_t)i * W;
+      for (int q = 0; q < W; ++q) row[q] = 0;
+      const int32_t c = m[i];
+      for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e) {
+        const int32_t r = A.row_idx[e];
+        for (int64_t f = A.rptr[r]; f < A.rptr[r + 1]; ++f) {
+          const int j = A.loc[A.rcols[f]];
+          if (j != i) row[j >> 6] |= 1ull << (j & 63);
+        }
+      }
+    }
+    const bool lds_rows = n * (K + 1) <= ILP_LRCAP;
+    if (lds_rows)
+      for (int t = lane; t < n * (K + 1); t += 64) lrs[t] = lrg[t];
+    const uint16_t* lr = lds_rows ? lrs : lrg;
+    wave_sync();
+    const int ow = (nrow + 63) / 64;
+    auto bound = [&](uint64_t P) {
+      for (int q = lane; q < ow; q += 64) open[q] = 0;
+      __builtin_amdgcn_wave_barrier();
+      double s = 0.0;
+      for (int q = 0; q < W; ++q) {
+        const uint64_t word = __shfl(P, q, 64);
+        if (word == 0) continue;
+        const int i = q * 64 + lane;
+        bool pend = (word >> lane) & 1;
+        uint16_t rr[8];
+        uint16_t o = 0;
+        if (pend) {
+          const uint16_t* li = lr + i * (K + 1);
+          bool cov = false;
+#pragma unroll
+          for (int a = 0; a < 8; ++a) {
+            rr[a] = a < K ? li[a] : li[0];
+            cov |= (open[rr[a] >> 6] >> (rr[a] & 63)) & 1;
+          }
+          o = li[K];
+          pend = !cov;
+        }
+        for (;;) {
+          const uint64_t bal = __ballot(pend);
+          if (bal == 0) break;
+          const int f = __builtin_ctzll(bal);
+          const int ob = __shfl((int)o, f, 64);
+          s += wl[q * 64 + f];
+          if (lane == f) {
+            open[ob >> 6] |= 1ull << (ob & 63);
+            pend = false;
+          }
+          if (pend) {
+#pragma unroll
+            for (int a = 0; a < 8; ++a) pend = pend && rr[a] != ob;
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      return s;
+    };
+    // lane-sliced sets: P (candidates), chosen
+    uint64_t P = 0, chosen = 0, best_set = 0;
+    if (lane < W) P = (lane == W - 1 && (n & 63)) ? ((1ull << (n & 63)) - 1) : ~0ull;
+    double best = -1.0, cur = 0.0;
+    int depth = 0;
+    int64_t nodes = 0;
+    bool exact = true;
+    for (;;) {
+      bool back = false;
+      if (++nodes > A.node_limit) { exact = false; break; }
+      const uint64_t nz = __ballot(P != 0);
+      if (nz == 0) {
+        if (cur > best) { best = cur; best_set = chosen; }
+        back = true;
+      } else if (cur + bound(P) <= best) {
+        back = true;
+      } else {
+        const int fl = __builtin_ctzll(nz);
+        const uint64_t pw = __shfl(P, fl, 64);
+        const int j = fl * 64 + __builtin_ctzll(pw);
+        uint64_t* fr = stk + (int64_t)depth * (W + 2);
+        if (lane < W) fr[lane] = P;
+        if (lane == 0) {
+          fr[W] = (uint64_t)__double_as_longlong(cur);
+          fr[W + 1] = ((uint64_t)j << 1) | 1u;
+        }
+        ++depth;
+        const uint64_t aw = lane < W ? adj[(int64_t)j * W + lane] : 0;
+        P &= ~aw;
+        if (lane == (j >> 6)) {
+          P &= ~(1ull << (j & 63));
+          chosen |= 1ull << (j & 63);
+        }
+        cur += wl[j];
+      }
+      if (back) {
+        bool found = false;
+        wave_sync();
+        while (depth > 0) {
+          uint64_t* fr = stk + (int64_t)(depth - 1) * (W + 2);
+          const uint64_t f = fr[W + 1];
+          const int j = (int)(f >> 1);
+          if (f & 1u) {
+            wave_sync();
+            if (lane == 0) fr[W + 1] = (uint64_t)j << 1;
+            P = lane < W ? fr[lane] : 0;
+            cur = __longlong_as_double((long long)fr[W]);
+            // candidates chosen below this frame are all > j (heavier ones come first)
+            if (lane == (j >> 6)) {
+              P &= ~(1ull << (j & 63));
+              chosen &= (1ull << (j & 63)) - 1;
+            } else if (lane > (j >> 6)) {
+              chosen = 0;
+            }
+            found = true;
+            break;
+          }
+          --depth;
+        }
+        if (!found) break;
+      }
+    }
+    // x: lane l owns members 64 l .. 64 l + 63
+    if (lane < W) {
+      for (int b = 0; b < 64; ++b) {
+        const int i = lane * 64 + b;
+        if (i >= n) break;
+        A.x[m[i]] = (best_set >> b) & 1 ? 1 : 0;
+        A.exact[m[i]] = exact ? 1 : 0;
+      }
+    }
+    wave_sync();
+  }
+}
+
+int ilp_small_max() { return ILP_SMALL; }
+int ilp_big_max() { return ILP_BIG; }
+
+void launch_ilp(hipStream_t stream, int phase, const IlpArgs& A, int n_big, int n_waves) {
+  const int64_t nbc = (A.n_cols + ILP_WG - 1) / ILP_WG;
+  const int64_t nbk = (A.n_comp + ILP_WG - 1) / ILP_WG;
+  switch (phase) {
+    case 0:
+      if (A.n_cols > 0 || A.n_rows > 0) {
+        const int64_t nbi = ((A.n_cols > A.n_rows ? A.n_cols : A.n_rows) + ILP_WG - 1) / ILP_WG;
+        hipLaunchKernelGGL(k_ilp_init, dim3(nbi), dim3(ILP_WG), 0, stream, A);
+      }
+      if (nbc) {
+        hipLaunchKernelGGL(k_ilp_rep, dim3(nbc), dim3(ILP_WG), 0, stream, A);
+        hipLaunchKernelGGL(k_ilp_union, dim3(nbc), dim3(ILP_WG), 0, stream, A);
+        hipLaunchKernelGGL(k_ilp_root, dim3(nbc), dim3(ILP_WG), 0, stream, A);
+      }
+      break;
+    case 1:
+      if (nbc) hipLaunchKernelGGL(k_ilp_csize, dim3(nbc), dim3(ILP_WG), 0, stream, A);
+      break;
+    case 2:
+      if (nbc) hipLaunchKernelGGL(k_ilp_fill, dim3(nbc), dim3(ILP_WG), 0, stream, A);
+      break;
+    case 3:
+      if (nbk) {
+        hipLaunchKernelGGL(k_ilp_small, dim3(nbk), dim3(ILP_WG), 0, stream, A);
+        hipLaunchKernelGGL(k_ilp_biglist, dim3(nbk), dim3(ILP_WG), 0, stream, A);
+      }
+      break;
+    case 4:
+      if (n_big > 0) hipLaunchKernelGGL(k_ilp_wave, dim3(n_waves), dim3(64), 0, stream, A, n_big);
+      break;
+  }
+}
+
+}  // namespace rgc

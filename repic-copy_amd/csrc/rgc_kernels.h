@@ -204,4 +204,39 @@ struct ScoreArgs {
 int score_tile_words();
 void launch_score_raster(hipStream_t stream, int n_tiles, const ScoreArgs& A);
 
+// run_ilp exact set packing (rgc_ilp.hip)
+struct IlpArgs {
+  int64_t n_cols, n_rows, n_comp;
+  int kmax;                   // largest number of rows of a column
+  int64_t node_limit;         // branch-and-bound nodes per component
+  const int64_t* col_ptr;     // [n_cols + 1] CSC
+  const int32_t* row_idx;     // global row ids
+  const double* w;            // [n_cols]
+  int32_t* rep;               // [n_rows] smallest column of each row
+  int32_t* rloc;              // [n_rows] solvers: winning member slot of each row
+  int32_t* parent;            // [n_cols]
+  int32_t* is_root;           // [n_cols]
+  int32_t* csize;             // [n_cols] component size by root
+  int32_t* rcnt;              // [n_rows] columns per row
+  int32_t* rcur;              // [n_rows]
+  const int64_t* rptr;        // [n_rows + 1] scanned rcnt
+  int32_t* rcols;             // [nnz] columns of each row
+  const int64_t* comp_id;     // [n_cols] scanned is_root (valid on roots)
+  int32_t* comp_n;            // [n_comp]
+  const int64_t* comp_off;    // [n_comp + 1]
+  int32_t* comp_cur;          // [n_comp]
+  int32_t* members;           // [n_cols] by component
+  int32_t* loc;               // [n_cols] local index in its component
+  uint64_t* scratch;          // small solver: (2 kmax + 8) words per column
+  int32_t* big;               // components for the wave solver
+  unsigned int* n_big;
+  uint64_t* wscratch;         // wave solver: wstride words per wave
+  int64_t wstride;
+  uint8_t* x;                 // [n_cols] solution
+  uint8_t* exact;             // [n_cols] 1 = component proven optimal
+};
+int ilp_small_max();
+int ilp_big_max();
+void launch_ilp(hipStream_t stream, int phase, const IlpArgs& A, int n_big, int n_waves);
+
 }  // namespace rgc

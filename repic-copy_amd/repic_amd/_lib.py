@@ -81,7 +81,7 @@ lib.rgc_test_epilogue.argtypes = [C.c_int, _f64p, _f64p, _f64p, C.POINTER(C.c_in
 EXPORTS = ["rgc_abi_version", "rgc_last_error", "rgc_device_count", "rgc_ctx_create",
            "rgc_ctx_destroy", "rgc_run", "rgc_kernel_times", "rgc_last_edges", "rgc_parse_files",
            "rgc_parsed_free", "rgc_py_hash_node", "rgc_py_set_order", "rgc_test_epilogue",
-           "rgc_score_pairs"]
+           "rgc_score_pairs", "rgc_ilp_solve"]
 
 
 class RGCError(RuntimeError):

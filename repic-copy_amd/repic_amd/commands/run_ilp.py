@@ -1,0 +1,114 @@
+"""``repic run_ilp`` — drop-in subcommand: the ILP consumer of get_cliques' outputs, with an
+exact set-packing solver on the MI355X instead of Gurobi.
+
+Same plugin protocol and arguments as the reference module (repic/commands/run_ilp.py:13-26):
+``in_dir``, ``box_size``, ``--num_particles``.  Reads the same four pickles per micrograph
+(:29-42,72-80), solves max w.x s.t. A x <= 1, x binary (:50-63) for every micrograph of the
+directory in one device batch (repic_amd.ilp), then writes what the reference writes, in its
+order: ``<base>.box`` (chosen cliques' consensus coordinates by decreasing confidence, rounded
+with np.rint, :112-124) and one more line of ``<base>_runtime.tsv`` (:127-131).
+
+Differences, stated: Gurobi stops at a 1e-4 relative MIP gap by default; this solver is exact
+(f32 weights summed in f64), and picks, among equally good packings, the one its
+heaviest-first branch order meets first (Gurobi's choice among ties is unspecified).  Lines
+of equal confidence follow our clique column order (the reference's is CPython set order,
+not reproducible, get_cliques.py:161).  A component that exceeds ``--node_limit`` keeps the
+best packing found and a warning names the micrograph.  With ``--multi_out`` inputs the
+reference raises AttributeError (``confidences`` is a tuple there, :97-106); so does this.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import pickle
+import sys
+import time
+
+import numpy as np
+
+from .. import _lib
+from ..ilp import solve_batch
+
+name = "run_ilp"
+
+
+def add_arguments(parser):
+    """Same CLI surface as the reference (run_ilp.py:16-23) plus tuning knobs."""
+    parser.add_argument("in_dir",
+                        help="path to input directory containing get_cliques.py output")
+    parser.add_argument("box_size", type=int,
+                        help="particle detection box size (in int[pixels])")
+    parser.add_argument("--num_particles", type=int,
+                        help="filter for the number of expected particles (int)")
+    parser.add_argument("--node_limit", type=int, default=0,
+                        help="branch-and-bound nodes per conflict component (0: 2^22)")
+    parser.add_argument("--device", type=int, default=None,
+                        help="HIP device (default: $LOCAL_RANK or 0)")
+
+
+def _load(path):
+    with open(path, "rb") as f:
+        return pickle.load(f)
+
+
+def main(args):
+    assert os.path.isdir(args.in_dir), "Error - input directory is missing"
+    files = glob.glob(os.path.join(args.in_dir, "*_constraint_matrix.pickle"))
+    dev = args.device if getattr(args, "device", None) is not None else \
+        int(os.environ.get("LOCAL_RANK", "0"))
+    # load every micrograph's matrix and weights in the reference's order; a failing load
+    # stops there, the earlier micrographs are still solved and written (as the reference
+    # would have written them before reaching it)
+    t0 = time.time()
+    mats, weights, err = [], [], None
+    for mf in files:
+        try:
+            A = _load(mf)
+            w = _load(mf.replace("_constraint_matrix", "_weight_vector"))
+        except Exception as e:  # noqa: BLE001 - re-raised at this micrograph
+            err = e
+            break
+        mats.append(A)
+        weights.append(w)
+    xs, exact = [], []
+    if mats:
+        ctx = _lib.Context(dev)
+        try:
+            xs, exact = solve_batch(ctx, mats, weights, getattr(args, "node_limit", 0))
+        finally:
+            ctx.close()
+    share = (time.time() - t0) / max(1, len(mats))
+    for i, mf in enumerate(files):
+        start = time.time()
+        base = os.path.basename(mf.replace("_constraint_matrix.pickle", ""))
+        print(f"\n--- {base} ---\n")
+        if i == len(mats):
+            raise err
+        A, x = mats[i], xs[i].astype(np.float64)
+        if not exact[i]:
+            print(f"Warning - {base}: node limit reached in a conflict component, the packing "
+                  f"is the best found (not proven optimal)", file=sys.stderr)
+        # run_ilp.py:66-69: every vertex at most once, and at least one clique chosen
+        assert np.max(A.tocsr() @ x) == 1, "Error - vertices are assigned to multiple cliques"
+        coords = _load(mf.replace("_constraint_matrix", "_consensus_coords"))
+        confidences = _load(mf.replace("_constraint_matrix", "_consensus_confidences"))
+        multi_out = type(coords[0][0]) == str
+        if multi_out:
+            coords = coords[1:]
+        cliques, confidences = zip(*[(coords[j], confidences[j]) for j in np.where(x == 1.)[0]])
+        if multi_out:
+            # run_ilp.py:97-106 extends the tuple ``confidences``
+            raise AttributeError("'tuple' object has no attribute 'extend'")
+        box_size = str(args.box_size)
+        out_file = mf.replace("_constraint_matrix.pickle", ".box")
+        lines = []
+        for j, (val, weight) in enumerate(sorted(zip(cliques, confidences), key=lambda t: t[1],
+                                                 reverse=True)):
+            if args.num_particles is None or j < args.num_particles:
+                lines.append("\t".join([str(int(np.rint(val[0]))), str(int(np.rint(val[1]))),
+                                        box_size, box_size, str(weight)]) + "\n")
+        with open(out_file, "wt") as o:
+            o.writelines(lines)
+        with open(mf.replace("_constraint_matrix.pickle", "_runtime.tsv"), "a") as o:
+            o.write(str(share + time.time() - start) + "\n")
+    sys.stdout.flush()

@@ -1,0 +1,173 @@
+"""run_ilp (reference repic/commands/run_ilp.py:25-136).
+
+The reference's Gurobi is not installed, so parity against it is UNPINNED; the device solver
+(rgc_ilp.hip) is checked against two independent exact solvers on the same model
+(oracle/ilp_ref.py: HiGHS with zero gap, and brute force per conflict component), on the
+constraint matrices the reference's get_cliques produced for the golden cases and on full-size
+synthetic C2/C3/C4 micrographs.  Objectives must be equal (f32 weights summed in f64 are exact;
+1e-12 relative allows for HiGHS' own summation); the packings must match wherever the optimum
+is unique.
+"""
+import argparse
+import os
+
+import numpy as np
+import pytest
+from scipy.sparse import coo_matrix
+
+from golden_util import load_case
+
+
+def golden_problems(name="c1_10017"):
+    meta, data = load_case(name)
+    out, r0, c0 = [], 0, 0
+    for g in meta["micrographs"]:
+        if g["status"] != "ok":
+            continue
+        V, C, k = g["V"], g["C"], g["k"]
+        rows = data["rows"][r0:r0 + C * k]
+        A = coo_matrix((np.ones(C * k, np.int64), (rows, np.repeat(np.arange(C), k))),
+                       shape=(V, C))
+        out.append((A, data["w"][c0:c0 + C].astype(np.float32)))
+        r0 += C * k
+        c0 += C
+    return out
+
+
+def synthetic_problems(cfg_name, n, seed=0):
+    from oracle import cpu_vec
+    from repic_amd import synth
+    cfg = synth.SynthConfig(**synth.CONFIGS[cfg_name], seed=seed)
+    out = []
+    for mg in synth.batch(cfg, n):
+        x, y, s = (np.concatenate([t[i] for t in mg]) for i in range(3))
+        o = cpu_vec.micrograph(x, y, s, [len(t[0]) for t in mg], cfg.box)
+        C = len(o["w"])
+        rows = o["rows"].reshape(-1)
+        A = coo_matrix((np.ones(len(rows), np.int64), (rows, np.repeat(np.arange(C), cfg.k))),
+                       shape=(o["V"], C))
+        out.append((A, o["w"]))
+    return out
+
+
+def test_milp_oracle_matches_brute_force_on_golden():
+    from oracle import ilp_ref
+    n = 0
+    for A, w in golden_problems():
+        bf = ilp_ref.brute_force(A, w)
+        if bf is None:
+            continue
+        x, obj = ilp_ref.milp(A, w)
+        assert ilp_ref.is_packing(A, x)
+        assert abs(obj - bf[1]) <= 1e-12 * max(1.0, obj)
+        n += 1
+    assert n >= 6
+
+
+def _check(problems, xs, exact, inexact_gap=None):
+    """Exact components must reach the optimum; with ``inexact_gap`` a micrograph whose solve
+    hit the node limit must be a packing within that relative gap of it."""
+    from oracle import ilp_ref
+    uniq, gaps = 0, []
+    for (A, w), x, ex in zip(problems, xs, exact):
+        assert ilp_ref.is_packing(A, x)
+        w64 = np.asarray(w, np.float64)
+        obj = float(np.sum(w64[x == 1]))
+        xr, objr = ilp_ref.milp(A, w)
+        if not ex:
+            assert inexact_gap is not None
+            gaps.append((objr - obj) / objr)
+            assert -1e-12 <= gaps[-1] <= inexact_gap, (obj, objr)
+            continue
+        assert abs(obj - objr) <= 1e-12 * max(1.0, objr), (obj, objr)
+        if np.array_equal(x, xr):
+            uniq += 1
+    print("inexact micrographs:", len(gaps), "relative gaps:", gaps)
+    return uniq
+
+
+@pytest.mark.gpu
+def test_gpu_ilp_matches_exact_solvers_on_golden():
+    from repic_amd import _lib
+    from repic_amd.ilp import solve_batch
+    probs = golden_problems() + golden_problems("syn_k4") + golden_problems("syn_k5")
+    ctx = _lib.Context(0)
+    xs, exact = solve_batch(ctx, [a for a, _ in probs], [w for _, w in probs])
+    ctx.close()
+    assert _check(probs, xs, exact) >= len(probs) - 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg_name,n,gap", [("C2", 60, None), ("C4", 20, None), ("C3", 3, 0.01)])
+def test_gpu_ilp_matches_exact_solvers_synthetic(cfg_name, n, gap):
+    """Full-size micrographs; C3/C4 have conflict components of hundreds of cliques, which
+    take the wavefront solver.  C3's crowded components (~800 cliques) can exceed the node
+    limit: then the packing must be flagged inexact and be within 1 % of the optimum."""
+    from repic_amd import _lib
+    from repic_amd.ilp import solve_batch
+    probs = synthetic_problems(cfg_name, n)
+    ctx = _lib.Context(0)
+    xs, exact = solve_batch(ctx, [a for a, _ in probs], [w for _, w in probs],
+                            node_limit=1 << 18 if gap else 0)
+    ctx.close()
+    _check(probs, xs, exact, gap)
+
+
+@pytest.mark.gpu
+def test_gpu_run_ilp_cli_on_get_cliques_output(tmp_path):
+    """get_cliques then run_ilp through the dispatcher (python -m repic_amd.main): the .box
+    files hold the optimal packing's consensus coordinates by decreasing confidence."""
+    import pickle
+    import subprocess
+    import sys
+
+    from golden_util import make_inputs
+    from oracle import ilp_ref
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    in_dir = make_inputs("c1_10017", str(tmp_path))
+    out = str(tmp_path / "out")
+    env = dict(os.environ, PYTHONPATH=os.path.join(root, "repic-copy_amd"))
+    for cmd in (["get_cliques", in_dir, out, "180"], ["run_ilp", out, "180"]):
+        r = subprocess.run([sys.executable, "-m", "repic_amd.main"] + cmd, env=env,
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-3000:]
+    mats = sorted(f for f in os.listdir(out) if f.endswith("_constraint_matrix.pickle"))
+    assert mats
+    for mf in mats:
+        base = mf[:-len("_constraint_matrix.pickle")]
+        ld = lambda s: pickle.load(open(os.path.join(out, base + s), "rb"))  # noqa: E731
+        A, w = ld("_constraint_matrix.pickle"), ld("_weight_vector.pickle")
+        coords, conf = ld("_consensus_coords.pickle"), ld("_consensus_confidences.pickle")
+        x, _ = ilp_ref.milp(A, w)
+        want = sorted(((int(np.rint(coords[j][0])), int(np.rint(coords[j][1])), str(conf[j]))
+                       for j in np.flatnonzero(x)), key=lambda t: (-float(t[2]), t))
+        got = [ln.split("\t") for ln in open(os.path.join(out, base + ".box")).read().splitlines()]
+        assert all(g[2] == g[3] == "180" for g in got)
+        confs = [float(g[4]) for g in got]
+        assert confs == sorted(confs, reverse=True)
+        assert sorted((int(g[0]), int(g[1]), g[4]) for g in got) == sorted(want)
+        lines = open(os.path.join(out, base + "_runtime.tsv")).read().splitlines()
+        assert len(lines) == 2 and float(lines[1]) >= 0
+
+
+@pytest.mark.gpu
+def test_gpu_run_ilp_num_particles_and_multi_out(tmp_path):
+    from golden_util import make_inputs
+    from repic_amd.commands import get_cliques, run_ilp
+    in_dir = make_inputs("c1_10017", str(tmp_path))
+    out = str(tmp_path / "out")
+    ga = argparse.Namespace(in_dir=in_dir, out_dir=out, box_size=180, multi_out=False,
+                            get_cc=False, batch_boxes=1 << 25, threads=None, device=None,
+                            listing=None)
+    get_cliques.main(ga)
+    run_ilp.main(argparse.Namespace(in_dir=out, box_size=180, num_particles=7, node_limit=0,
+                                    device=None))
+    for f in os.listdir(out):
+        if f.endswith(".box"):
+            assert len(open(os.path.join(out, f)).read().splitlines()) <= 7
+    ga.multi_out = True
+    ga.out_dir = out2 = str(tmp_path / "out2")
+    get_cliques.main(ga)
+    with pytest.raises(AttributeError):
+        run_ilp.main(argparse.Namespace(in_dir=out2, box_size=180, num_particles=None,
+                                        node_limit=0, device=None))
