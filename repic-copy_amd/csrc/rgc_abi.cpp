@@ -86,10 +86,11 @@ struct Buf {
 constexpr int LDS_BLOCK = 1280;
 constexpr int LDS_BLOCKS = 128;
 constexpr int FUSED_WG = 512;
-// Micrographs above this many boxes go straight to the large-micrograph route: at ~4k boxes
-// the fused kernel's LDS leaves room for ~2 edges per box, fewer than crowded micrographs
-// have (C3: 3.8), so the fused attempt would only defer them after its pair pass.
-constexpr int64_t FUSED_MAX_BOXES = 3072;
+// Micrographs above this many boxes go straight to the large-micrograph route.  Above 2048
+// boxes the fused layout uses 2 n grid cells and u16 parents (29 B per box + 2 B per edge),
+// so a 4096-box micrograph (C3: ~4k boxes, ~15k edges) runs in one workgroup per CU with room
+// for 22k edges; at 4608 boxes ~13k edges still fit.
+constexpr int64_t FUSED_MAX_BOXES = 4608;
 // device cursors after the per-micrograph block: [0] clique reservation, [1] edges of finished
 // micrographs, [2] edge-dump reservation (RGC_F_EDGES), [3] spare
 constexpr size_t CUR_BYTES = 32;

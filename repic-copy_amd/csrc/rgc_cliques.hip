@@ -293,8 +293,9 @@ __global__ __launch_bounds__(WG) void k5_epilogue(CliqueArgs A) {
   int arg = 0;
   bool exact = multi;
   if (!multi) {
-    // weighted degrees from f32 JIs (error < 2e-6 per sum): a clear maximum is the
-    // reference's; anything within 1e-5 takes the exact f64 pass (ties included)
+    // weighted degrees from f32 JIs: f32 operands (2^-24 each) and v_rcp_f32 (1 ulp) give
+    // < 4e-7 per JI <= 1, < 5.5e-6 per sum of <= 7 terms with its f32 additions; a maximum
+    // clear by 3e-5 is the reference's, anything closer takes the exact f64 pass (ties)
     float deg[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) deg[i] = 0.0f;
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(WG) void k5_epilogue(CliqueArgs A) {
     for (int a = 0; a < K; ++a)
 #pragma unroll
       for (int b = a + 1; b < K; ++b) {
-        const float jf = (float)I[t] / (float)(two_b2 - I[t]);
+        const float jf = (float)I[t] * __builtin_amdgcn_rcpf((float)(two_b2 - I[t]));
         deg[a] += jf;
         deg[b] += jf;
         ++t;
@@ -316,7 +317,7 @@ __global__ __launch_bounds__(WG) void k5_epilogue(CliqueArgs A) {
       arg = d > d1 ? i : arg;
       d1 = fmaxf(d1, d);
     }
-    exact = !(d1 - d2 > 1e-5f);
+    exact = !(d1 - d2 > 3e-5f);
   }
   // median JI = JI of the median overlap (JI is non-decreasing in I and the f64 quotient
   // keeps that order): one or two reference divisions; I is sorted in place

@@ -53,6 +53,10 @@ struct FusedHdr {
   int64_t C, base;
 };
 
+// cell budget (keys over all pickers' grids) of a size class: 4 n up to 2048 boxes; 2 n above,
+// where LDS is the limit (one workgroup per CU) and larger cells only cost P2 candidates
+__host__ __device__ inline int fused_cells(int nmax) { return nmax <= 2048 ? 4 * nmax : 2 * nmax; }
+
 // wide: f64 coordinates in LDS; otherwise f32 (every coordinate of the micrograph is exactly
 // representable as f32, checked in P0, so the f64 values are recovered exactly)
 __host__ __device__ inline FusedLayout fused_layout(int nmax, int ecap, bool wide) {
@@ -69,8 +73,8 @@ __host__ __device__ inline FusedLayout fused_layout(int nmax, int ecap, bool wid
   // P1-P3 grid and union-find; the cell starts (dead after P2) become the clique buffer of
   // P4-P6, parent..scell (dead after P5) the f64 scores of P6
   L.off_union = o;
-  L.off_cstart = o; o += al(2 * (4 * nmax + 8));   // u16 cell starts, <= 4n + 1 cells
-  L.off_parent = o; o += al(4 * (nmax + 4));
+  L.off_cstart = o; o += al(2 * (fused_cells(nmax) + 8));   // u16 cell starts
+  L.off_parent = o; o += al(2 * (nmax + 8));    // u16 union-find parents; P5 u16 bucket counts
   L.off_scell = o; o += al(2 * nmax);         // sorted position -> cell
   L.off_citems = o; o += al(2 * nmax);        // sorted position -> local box index
   L.off_flags = o; o += al(nmax);             // by local index: 1 graph node, 3 clique vertex
@@ -87,7 +91,7 @@ struct FShared {
   uint16_t* cstart;
   uint32_t* cnt;
   uint16_t* fwd;
-  uint32_t* parent;
+  uint16_t* parent;
   uint16_t* citems;
   uint16_t* pos;
   uint16_t* scell;
@@ -150,23 +154,36 @@ __device__ __forceinline__ uint32_t lds_ld(uint32_t* p) {
 __device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-__device__ __forceinline__ uint32_t uf_find_lds(uint32_t* parent, uint32_t x) {
+__device__ __forceinline__ uint32_t p16_ld(uint16_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void p16_st(uint16_t* p, uint32_t v) {
+  __hip_atomic_store(p, (uint16_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// u16 parents (positions < 2^16), path halving
+__device__ __forceinline__ uint32_t uf_find_lds(uint16_t* parent, uint32_t x) {
   for (;;) {
-    const uint32_t p = lds_ld(parent + x);
+    const uint32_t p = p16_ld(parent + x);
     if (p == x) return x;
-    const uint32_t gp = lds_ld(parent + p);
-    if (gp != p) lds_st(parent + x, gp);
+    const uint32_t gp = p16_ld(parent + p);
+    if (gp != p) p16_st(parent + x, gp);
     x = gp;
   }
 }
-// lock-free union (link the larger root under the smaller), workgroup-scope LDS atomics
-__device__ __forceinline__ void uf_union_lds(uint32_t* parent, uint32_t a, uint32_t b) {
+// lock-free union (link the larger root under the smaller): CAS on the 32-bit word holding
+// the root's u16 entry (a concurrent store to the other half only makes the CAS retry)
+__device__ __forceinline__ void uf_union_lds(uint16_t* parent, uint32_t a, uint32_t b) {
   for (;;) {
     a = uf_find_lds(parent, a);
     b = uf_find_lds(parent, b);
     if (a == b) return;
     if (a < b) { const uint32_t t = a; a = b; b = t; }
-    if (atomicCAS(&parent[a], a, b) == a) return;
+    uint32_t* wp = reinterpret_cast<uint32_t*>(parent) + (a >> 1);
+    const int sh = 16 * (a & 1);
+    const uint32_t w = lds_ld(wp);
+    if (((w >> sh) & 0xFFFFu) != a) continue;   // a was linked meanwhile
+    const uint32_t nw = (w & ~(0xFFFFu << sh)) | (b << sh);
+    if (atomicCAS(wp, w, nw) == w) return;
   }
 }
 
@@ -354,8 +371,9 @@ __device__ __forceinline__ bool fused_epilogue_main(const FCtx<K>& c, int64_t j,
     for (int i = 0; i < K; ++i) c.members[j * K + i] = c.b0 + li[i];
   }
   if (c.flags & 2) return true;
-  // weighted degrees from f32 JIs (error < 2e-6 absolute per sum): a clear maximum is the
-  // reference's; anything within 1e-5 goes to the exact f64 pass (ties included)
+  // weighted degrees from f32 JIs: f32 operands (2^-24 each) and v_rcp_f32 (1 ulp) give
+  // < 4e-7 per JI <= 1, < 5.5e-6 per sum of <= 7 terms with its f32 additions; a maximum
+  // clear by 3e-5 is the reference's, anything closer goes to the exact f64 pass (ties)
   float deg[K];
 #pragma unroll
   for (int i = 0; i < K; ++i) deg[i] = 0.0f;
@@ -365,7 +383,7 @@ __device__ __forceinline__ bool fused_epilogue_main(const FCtx<K>& c, int64_t j,
     for (int a = 0; a < K; ++a)
 #pragma unroll
       for (int b = a + 1; b < K; ++b) {
-        const float jf = (float)I[t] / (float)(c.two_b2 - I[t]);
+        const float jf = (float)I[t] * __builtin_amdgcn_rcpf((float)(c.two_b2 - I[t]));
         deg[a] += jf;
         deg[b] += jf;
         ++t;
@@ -380,7 +398,7 @@ __device__ __forceinline__ bool fused_epilogue_main(const FCtx<K>& c, int64_t j,
     arg = d > d1 ? i : arg;
     d1 = fmaxf(d1, d);
   }
-  if (!(d1 - d2 > 1e-5f)) return true;
+  if (!(d1 - d2 > 3e-5f)) return true;
   int cons = li[0];
 #pragma unroll
   for (int i = 1; i < K; ++i) cons = (arg == i) ? li[i] : cons;
@@ -850,7 +868,7 @@ void k_fused(FusedArgs A) {
   S.split = reinterpret_cast<uint16_t*>(smem + L.off_scell);
   S.vscore = reinterpret_cast<double*>(smem + L.off_parent);
   S.vstaged = false;
-  S.parent = reinterpret_cast<uint32_t*>(smem + L.off_parent);
+  S.parent = reinterpret_cast<uint16_t*>(smem + L.off_parent);
   S.citems = reinterpret_cast<uint16_t*>(smem + L.off_citems);
   S.pos = reinterpret_cast<uint16_t*>(smem + L.off_pos);
   S.scell = reinterpret_cast<uint16_t*>(smem + L.off_scell);
@@ -966,7 +984,7 @@ void k_fused(FusedArgs A) {
       if (!(ex < 0x1p40 && ey < 0x1p40)) {
         H.cell = INFINITY; H.gx = 1; H.gy = 1;
       } else {
-        const double budget = (double)((4 * A.nmax + 4) / K);
+        const double budget = (double)((fused_cells(A.nmax) + 4) / K);
         double cl = fmax(0.54 * A.B, fmax(sqrt(ex * ey / budget), fmax(ex, ey) / budget));
         for (;;) {
           const double fx = floor(ex / cl) + 1.0, fy = floor(ey / cl) + 1.0;
@@ -1106,6 +1124,7 @@ void k_fused(FusedArgs A) {
       }
     }
     __syncthreads();
+    STAMP(5);   // fill
     if (src_ok) {
       for (int e = tid; e < E; e += FWG) {
         const uint32_t h = S.dst[e];
@@ -1134,7 +1153,6 @@ void k_fused(FusedArgs A) {
       __syncthreads();
       if (tid == 0) H.base = 0;
     }
-    STAMP(5);   // fill + sort
   }
   if (H.status != 0) {
     if (tid == 0) put_stats(A, m, H.status, H.E, 0, 0, 0, 0, 0, 0);
@@ -1144,13 +1162,13 @@ void k_fused(FusedArgs A) {
   STOP_AFTER(2);
   
   // ---- P3: connected components: the unions ran in the P2 fill; compress, count sizes
-  STAMP(6);   // (empty: union fused into the fill)
+  STAMP(6);   // union (one thread per edge)
   for (int i = tid; i < n; i += FWG) {
     if (!S.flags[i]) continue;
     const int e0 = S.fwd[i], e1 = S.fwd[i + 1];
     S.split[i] = (uint16_t)lb16(S.dst, e0, e1, next_picker_end<K>(c.pp, i));   // every node
     const uint32_t r = uf_find_lds(S.parent, i);
-    lds_st(S.parent + i, r);
+    p16_st(S.parent + i, r);
     atomicAdd(&ccsz[r >> 1], 1u << (16 * (r & 1)));
   }
   __syncthreads();
@@ -1304,19 +1322,24 @@ void k_fused(FusedArgs A) {
   // the bucket.  The grid arrays of P1 are dead: parent holds the bucket counters, scell the
   // vertices (sorted positions) in bucket order.
   if (H.status == 0) {
-    uint32_t* bcnt = S.parent;
+    // bucket counts as packed u16 (two per LDS word; a bucket holds < 2^16 vertices) in the
+    // dead union-find parents
+    uint16_t* bcnt = S.parent;
+    uint32_t* bw = reinterpret_cast<uint32_t*>(S.parent);
     uint16_t* blist = S.scell;
     const double minx = H.minx, xbs = H.xbs;
     auto xbucket = [&](double xv) { return (int)fmin((xv - minx) * xbs, (double)(n - 1)); };
-    for (int q = tid; q <= n; q += FWG) bcnt[q] = 0;
+    for (int q = tid; q <= (n + 1) / 2; q += FWG) bw[q] = 0;
     __syncthreads();
     for (int t = tid; t < n; t += FWG) {
       if (S.flags[t] != 3) continue;
-      S.vrank[t] = (uint16_t)atomicAdd(&bcnt[xbucket(ld_xy<W>(S, t).x)], 1u);
+      const int q = xbucket(ld_xy<W>(S, t).x);
+      const int sh = 16 * (q & 1);
+      S.vrank[t] = (uint16_t)((atomicAdd(&bw[q >> 1], 1u << sh) >> sh) & 0xFFFFu);
     }
     __syncthreads();
-    const int64_t V = block_scan_array<FWG>(bcnt, n, H.red64);
-    if (tid == 0) { H.V = (int)V; bcnt[n] = (uint32_t)V; }
+    const int64_t V = block_scan_u16<FWG>(bcnt, n, H.red64);
+    if (tid == 0) { H.V = (int)V; bcnt[n] = (uint16_t)V; }
     for (int t = tid; t < n; t += FWG) {
       if (S.flags[t] != 3) continue;
       blist[bcnt[xbucket(ld_xy<W>(S, t).x)] + S.vrank[t]] = (uint16_t)t;

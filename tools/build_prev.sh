@@ -1,22 +1,22 @@
 #!/bin/bash
-# Build the fused kernel of a previous commit (default HEAD) as ablate/librepic_gc_zprev.so, so
+# Build a previous commit's library (default HEAD) as ablate/librepic_gc_zprev.so, so
 # tools/ablate.py times it interleaved with the working tree's build on the same box and clock.
 #   bash tools/build_prev.sh [REV]
 set -e
 REV=${1:-HEAD}
 D=repic-copy_amd/csrc
+rm -rf $D/build/prev
 mkdir -p $D/build/prev repic-copy_amd/repic_amd/ablate
-for f in rgc_fused.hip rgc_abi.cpp rgc_kernels.hip rgc_kernels.h rgc_device.h pyset.h box_parse.cpp; do
+for f in $(git ls-tree --name-only "$REV" $D/ | xargs -n1 basename); do
   git show "$REV:$D/$f" > $D/build/prev/$f
 done
 git show "$REV:include/repic_gc.h" > $D/build/prev/repic_gc.h
 H="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wno-unused-function -munsafe-fp-atomics"
 cd $D/build/prev
 sed -i 's#"../../include/repic_gc.h"#"repic_gc.h"#' *.cpp *.hip *.h
-/opt/rocm/bin/hipcc $H -c rgc_fused.hip -o f.o &
-/opt/rocm/bin/hipcc $H -c rgc_kernels.hip -o k.o &
-g++ -O2 -std=c++17 -fPIC -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -c rgc_abi.cpp -o a.o &
-g++ -O2 -std=c++17 -fPIC -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -c box_parse.cpp -o b.o &
+objs=""
+for f in *.hip; do /opt/rocm/bin/hipcc $H -c $f -o ${f%.hip}.o & objs="$objs ${f%.hip}.o"; done
+for f in *.cpp; do g++ -O2 -std=c++17 -fPIC -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -c $f -o ${f%.cpp}.o & objs="$objs ${f%.cpp}.o"; done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../../repic_amd/ablate/librepic_gc_zprev.so f.o k.o a.o b.o -lpthread
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../../repic_amd/ablate/librepic_gc_zprev.so $objs -lpthread
 echo "built ablate/librepic_gc_zprev.so from $REV"

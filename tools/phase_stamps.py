@@ -35,7 +35,7 @@ n = f(ctx._p, None, 0)
 buf = (C.c_uint64 * n)()
 f(ctx._p, buf, n)
 st = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 16).astype(np.int64)[:, :13]
-names = ["P0 load+bbox", "P1 grid+sort", "P2a count", "P2b fwd scan", "P2c fill+sort",
+names = ["P0 load+bbox", "P1 grid+sort", "P2a count", "P2b fwd scan", "P2c fill",
          "P3a union", "P3b CC stats", "P4a DFS+queue", "P4b scan+reserve", "P5 rank",
          "P6a score staging", "P6b epilogue"]
 valid = (st != 0).all(axis=1)
