@@ -149,7 +149,12 @@ static const FusedPlan& cached_plan(int k, int pass, int nmax) {
   auto it = memo.find({k, pass, nmax});
   if (it != memo.end()) return it->second;
   FusedPlan p;
-  if (!plan_fused(k, pass > 0, nmax, pass == 2 ? 1 : LDS_BLOCKS, &p)) p = FusedPlan();
+  // RGC_DIAG_MAX_WG: occupancy experiments only (caps workgroups per CU; outputs unchanged)
+  static const int diag_wg = [] {
+    const char* e = getenv("RGC_DIAG_MAX_WG");
+    return e ? std::max(1, atoi(e)) : LDS_BLOCKS;
+  }();
+  if (!plan_fused(k, pass > 0, nmax, pass == 2 ? 1 : diag_wg, &p)) p = FusedPlan();
   return memo.emplace(std::make_tuple(k, pass, nmax), p).first->second;
 }
 

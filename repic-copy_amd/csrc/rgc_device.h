@@ -67,6 +67,80 @@ __device__ __forceinline__ uint64_t block_min_u64(uint64_t v, uint64_t* lds) {
   return r;
 }
 
+// ----------------------------------------------------------------------------- DPP wave scans
+// gfx9 wave64 Hillis-Steele scan on DPP lane moves: row_shr:1/2/4/8 inside each 16-lane row,
+// then row_bcast:15 (lane 15 of a row to the next row) and row_bcast:31 (lane 31 to rows 2-3).
+// VALU only: no ds_bpermute round trips through the LDS crossbar.  64-bit values move as two
+// 32-bit halves.
+template <int CTRL, typename T>
+__device__ __forceinline__ T dpp_mov(T v) {
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32- or 64-bit lanes");
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(
+        T, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+  } else {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xf,
+                                                               0xf, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL,
+                                                               0xf, 0xf, false);
+    return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
+  }
+}
+// inclusive scan across the wave with an associative, commutative op (lane 63: the total)
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_incl_scan(T v, Op op) {
+  const int lane = threadIdx.x & 63, rl = lane & 15;
+  T t;
+  t = dpp_mov<0x111>(v); if (rl >= 1) v = op(t, v);
+  t = dpp_mov<0x112>(v); if (rl >= 2) v = op(t, v);
+  t = dpp_mov<0x114>(v); if (rl >= 4) v = op(t, v);
+  t = dpp_mov<0x118>(v); if (rl >= 8) v = op(t, v);
+  t = dpp_mov<0x142>(v); if (lane & 16) v = op(t, v);
+  t = dpp_mov<0x143>(v); if (lane >= 32) v = op(t, v);
+  return v;
+}
+
+// Exclusive scan of one value per thread across the workgroup on DPP wave scans.  ONE barrier:
+// the caller guarantees a barrier between any earlier use of lds and this call.
+template <int BS, typename T>
+__device__ __forceinline__ T block_excl_scan_dpp(T v, T* lds, T* total) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const T inc = wave_incl_scan(v, [](T a, T b) { return a + b; });
+  if (l == 63) lds[w] = inc;
+  __syncthreads();
+  T pre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < BS / 64; ++i) {
+    const T x = lds[i];
+    pre += (i < w) ? x : (T)0;
+    tot += x;
+  }
+  *total = tot;
+  return pre + inc - v;
+}
+
+// In-place exclusive scan of a[0..n) in LDS (each thread a contiguous chunk), a[n] = total,
+// ending with a barrier: two barriers in all, the caller guaranteeing one before (see above).
+// A = uint16_t (totals < 2^16) or uint32_t.
+template <int BS, typename A>
+__device__ __forceinline__ int64_t block_scan_dpp(A* a, int n, int64_t* lds) {
+  const int per = (n + BS - 1) / BS;
+  const int c0 = min((int)threadIdx.x * per, n), c1 = min(c0 + per, n);
+  int64_t s = 0;
+  for (int c = c0; c < c1; ++c) s += a[c];
+  int64_t tot;
+  int64_t pre = block_excl_scan_dpp<BS>(s, lds, &tot);
+  for (int c = c0; c < c1; ++c) {
+    const A v = a[c];
+    a[c] = (A)pre;
+    pre += v;
+  }
+  if (threadIdx.x == BS - 1) a[n] = (A)tot;
+  __syncthreads();
+  return tot;
+}
+
 // Exclusive scan of one value per thread across the workgroup.
 template <int BS = WG>
 __device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* lds, int64_t* total) {

@@ -576,7 +576,7 @@ struct BfsLevel {
       CN[e] = cnt;
     }
     __syncthreads();
-    const int64_t nN = block_scan_array<FWG>(CN, (int)nD, H.red64);
+    const int64_t nN = block_scan_dpp<FWG>(CN, (int)nD, H.red64);
     constexpr bool last = D + 1 == K;
     const int nb = (lvl[D] + 4 * (int)nD + 3) & ~3;   // next level starts here
     if (nN > 65535 || nN * (last ? 6 : 4) > tb - nb) { out.C = -1; return out; }
@@ -650,7 +650,7 @@ __device__ __forceinline__ BfsOut<K> bfs_cliques(const FShared& S, FusedHdr& H, 
     cnt[i] = root_ok(r) ? (uint32_t)(seg_end(r) - S.fwd[r]) : 0u;
   }
   __syncthreads();
-  const int64_t n2 = block_scan_array<FWG>(cnt, nr, H.red64);
+  const int64_t n2 = block_scan_dpp<FWG>(cnt, nr, H.red64);
   constexpr bool last = K == 2;
   if (n2 > 65535 || n2 * (last ? 6 : 4) > qbytes) return out;
   for (int i = tid; i < nr; i += FWG) {
@@ -946,13 +946,26 @@ void k_fused(FusedArgs A) {
     if (!W) inexact |= ((double)(float)xv != xv && xv == xv) || ((double)(float)yv != yv && yv == yv);
   });
   if (inexact) mnx = -INFINITY;   // (impossible otherwise) carried through the min reduction
+  // P1's packed bucket counters (the whole cell-start region of the size class), union-find
+  // parents, node flags and P2's packed CC-size counters are set up here, so the bounding-box
+  // barrier orders them too
+  {
+    uint32_t* cw = reinterpret_cast<uint32_t*>(S.cstart);
+    const int ncw = (fused_cells(A.nmax) + 8) / 2;
+    for (int q = tid; q < ncw; q += FWG) cw[q] = 0;
+    for (int i = tid; i < n; i += FWG) {
+      S.parent[i] = i;
+      S.flags[i] = 0;
+    }
+    uint32_t* ccsz = reinterpret_cast<uint32_t*>(S.vrank);
+    for (int q = tid; q < (n + 1) / 2; q += FWG) ccsz[q] = 0;
+  }
   {
     double v[4] = {mnx, mny, -mxx, -mxy};
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = fmin(v[r], __shfl_xor(v[r], o, 64));
-    if ((tid & 63) == 0)
+    for (int r = 0; r < 4; ++r)
+      v[r] = wave_incl_scan(v[r], [](double a, double b) { return fmin(a, b); });
+    if ((tid & 63) == 63)
 #pragma unroll
       for (int r = 0; r < 4; ++r) H.red4[r][tid >> 6] = v[r];
     __syncthreads();
@@ -975,78 +988,83 @@ void k_fused(FusedArgs A) {
   // an LDS counting sort of the boxes by (picker, cell).  JI > 0.3 implies I > (6/13) B^2 and
   // so |dx|, |dy| < (7/13) B = 0.5385 B: cells of side >= 0.54 B keep every edge inside the
   // 3x3 stencil, and per-picker grids let a box visit the boxes of higher pickers only.
-  if (tid == 0) {
-    H.minx = mnx; H.miny = mny; H.cell = A.B; H.inv_cell = 0.0; H.gx = 0; H.gy = 0; H.ncell = 0;
-    H.status = 0; H.C = 0; H.base = 0; H.V = 0; H.target = -1; H.ccur = 0;
-    H.tief[0] = H.tief[1] = 0;
+  // the grid is planned by every thread from the reduced bounding box (identical values, no
+  // thread-0 section and barrier); thread 0 only records what later phases read.  Planned in
+  // f32 with hardware reciprocals (every wave pays for it): exactness is not needed, only
+  // cells >= 0.54 B (0.28 % above the 7/13 B an edge needs, far above f32 rounding), K gx gy
+  // within the budget (checked on the integers used), and one inv_cell used by every key.
+  GridU G;
+  double xbs;
+  {
+    double cl = A.B, icl = 0.0;
+    int gx = 0, gy = 0;
     if (mnx <= mxx && A.B > 0.0) {
       const double ex = mxx - mnx, ey = mxy - mny;
       if (!(ex < 0x1p40 && ey < 0x1p40)) {
-        H.cell = INFINITY; H.gx = 1; H.gy = 1;
+        cl = INFINITY; gx = 1; gy = 1;
       } else {
-        const double budget = (double)((fused_cells(A.nmax) + 4) / K);
-        double cl = fmax(0.54 * A.B, fmax(sqrt(ex * ey / budget), fmax(ex, ey) / budget));
+        const int budget = (fused_cells(A.nmax) + 4) / K;
+        const float fex = (float)ex, fey = (float)ey, rb = __builtin_amdgcn_rcpf((float)budget);
+        float fcl = fmaxf((float)(0.54 * A.B) * 1.000001f,
+                          fmaxf(__builtin_sqrtf(fex * fey * rb), fmaxf(fex, fey) * rb));
         for (;;) {
-          const double fx = floor(ex / cl) + 1.0, fy = floor(ey / cl) + 1.0;
-          if (fx * fy <= budget) {
-            H.gx = (int)fx; H.gy = (int)fy;
+          const float ir = __builtin_amdgcn_rcpf(fcl);
+          const int fx = (int)floorf(fex * ir) + 1, fy = (int)floorf(fey * ir) + 1;
+          if (fx <= budget && fy <= budget && fx * fy <= budget) {
+            gx = fx; gy = fy;
             break;
           }
-          cl *= 1.0625;
+          fcl *= 1.0625f;
         }
-        H.cell = cl;
-        H.inv_cell = 1.0 / cl;
+        cl = (double)fcl;
+        icl = (double)__builtin_amdgcn_rcpf(fcl);
+        // keys use icl: a cell is 1 / icl wide, which must stay >= 0.54 B
+        if (icl * (0.54 * A.B) > 1.0) icl = 1.0 / (0.54 * A.B);
       }
-      H.ncell = H.gx * H.gy;
     }
-    H.nkey = K * H.ncell;
-    H.inv_gy = H.gy > 0 ? 1.0f / (float)H.gy : 0.0f;
+    G.minx = ufd(mnx); G.miny = ufd(mny); G.inv_cell = ufd(icl);
+    G.gx = ufl(gx); G.gy = ufl(gy); G.ncell = G.gx * G.gy; G.nkey = K * G.ncell;
+    G.inv_gy = G.gy > 0 ? __builtin_amdgcn_rcpf((float)G.gy) : 0.0f;
     const double ex = mxx - mnx;
-    H.xbs = (mnx < mxx && ex < 0x1p60) ? (double)n / ex : 0.0;
+    xbs = ufd((mnx < mxx && ex < 0x1p60) ? (double)((float)n * __builtin_amdgcn_rcpf((float)ex))
+                                         : 0.0);
+    if (tid == 0) {
+      H.minx = mnx; H.miny = mny; H.cell = cl; H.inv_cell = icl; H.gx = G.gx; H.gy = G.gy;
+      H.ncell = G.ncell; H.nkey = G.nkey; H.inv_gy = G.inv_gy; H.xbs = xbs;
+      H.status = 0; H.C = 0; H.base = 0; H.V = 0; H.target = -1; H.ccur = 0;
+      H.tief[0] = H.tief[1] = 0;
+    }
   }
-  __syncthreads();
-  const GridU G = grid_u(H);
   const int nk = G.nkey;
-  // counting sort by key with packed u16 counters (two keys per LDS word)
-  uint32_t* cw = reinterpret_cast<uint32_t*>(S.cstart);
-  for (int q = tid; q <= (nk + 2) / 2; q += FWG) cw[q] = 0;
-  // union-find and node flags for the P2 fill (by position; untouched until then)
-  for (int i = tid; i < n; i += FWG) {
-    S.parent[i] = i;
-    S.flags[i] = 0;
-  }
-  __syncthreads();
-  // counts go to slot key + 1, so the exclusive scan leaves bucket q's start in slot q + 1;
+  // counting sort by key with packed u16 counters (two keys per LDS word, zeroed in P0).
+  // Counts go to slot key + 1, so the exclusive scan leaves bucket q's start in slot q + 1;
   // the scatter's cursors advance it to bucket q's end = bucket q+1's start, which leaves
   // cstart[q] = start of bucket q for q = 0..nk+1 with no rebuild pass.  The key waits in
-  // pos[i] between the two passes.
+  // pos[i] between the passes.
+  uint32_t* cw = reinterpret_cast<uint32_t*>(S.cstart);
   each_box([&](int i, double xv, double yv) {
     const int q = box_key(G, picker_of<K>(c.pb, i), xv, yv) + 1;
     S.pos[i] = (uint16_t)q;
     atomicAdd(&cw[q >> 1], 1u << (16 * (q & 1)));
   });
   __syncthreads();
-  block_scan_u16<FWG>(S.cstart, nk + 2, H.red64);
+  block_scan_dpp<FWG>(S.cstart, nk + 2, H.red64);
+  // arrival order into fwd (free until P2), made deterministic by the placement pass
+  uint16_t* arrival = S.fwd;
   each_box([&](int i, double, double) {
     const int q = S.pos[i];
     const int sh = 16 * (q & 1);
     const int t = (atomicAdd(&cw[q >> 1], 1u << sh) >> sh) & 0xFFFF;
-    S.citems[t] = (uint16_t)i;   // arrival order, made deterministic below
+    arrival[t] = (uint16_t)i;
   });
   __syncthreads();
-  // deterministic order inside each bucket: by local index (buckets hold a few boxes)
-  uint16_t* tpos = S.vrank;   // final position of each box (vrank is free until P2)
-  each_box([&](int i, double, double) {
+  // placement: by local index inside each bucket (buckets hold a few boxes)
+  each_box([&](int i, double xv, double yv) {
     const int q = S.pos[i];
     const int lo = S.cstart[q - 1], hi = S.cstart[q];
     int t = lo;
-    for (int u = lo; u < hi; ++u) t += (int)S.citems[u] < i ? 1 : 0;
-    tpos[i] = (uint16_t)t;
-  });
-  __syncthreads();
-  each_box([&](int i, double xv, double yv) {
-    const int t = tpos[i];
-    S.scell[t] = (uint16_t)(S.pos[i] - 1);
+    for (int u = lo; u < hi; ++u) t += (int)arrival[u] < i ? 1 : 0;
+    S.scell[t] = (uint16_t)(q - 1);
     S.citems[t] = (uint16_t)i;
     S.pos[i] = (uint16_t)t;
     st_xy<W>(S, t, xv, yv);
@@ -1072,7 +1090,6 @@ void k_fused(FusedArgs A) {
   // picker K-1 have nothing to do.  cnt[] (dead until P3) keeps
   // each box's edge bitmask for the fill.
   uint32_t* ccsz = reinterpret_cast<uint32_t*>(S.vrank);   // packed u16 CC sizes (P2-P3)
-  for (int q = tid; q < (n + 1) / 2; q += FWG) ccsz[q] = 0;
   // boustrophedon box order: odd rounds walk their FWG positions backwards, so a thread that
   // took a low-picker box (most grids to search) in one round takes a high-picker box (fewest)
   // in the next; K = 3, ~900 boxes: at most 6 instead of 9 column ranges per thread
@@ -1088,16 +1105,15 @@ void k_fused(FusedArgs A) {
   __syncthreads();
   STAMP(3);   // count
   
-  const int64_t E = block_scan_u16<FWG>(S.fwd, n, H.red64);
+  // fwd[n] = E is written by the scan; the status is the same in every thread
+  const int E = (int)block_scan_dpp<FWG>(S.fwd, n, H.red64);
+  const int st2 = E == 0 ? RGC_ST_NO_EDGES : (E > A.ecap ? RGC_ST_DEFER : 0);
   if (tid == 0) {
-    S.fwd[n] = (uint16_t)E;
-    H.E = (int)E;
-    if (E == 0) H.status = RGC_ST_NO_EDGES;
-    else if (E > A.ecap) H.status = RGC_ST_DEFER;
+    H.E = E;
+    H.status = st2;
   }
-  __syncthreads();
   STAMP(4);   // scan
-  if (H.status == 0) {
+  if (st2 == 0) {
     // fill each list (already sorted: position order) and record each edge's source in dst's
     // unused tail when it has room; then union the edges one thread per edge (lock-free
     // union-find, balanced across lanes whatever the degrees).  Without room: union per box.
@@ -1154,8 +1170,8 @@ void k_fused(FusedArgs A) {
       if (tid == 0) H.base = 0;
     }
   }
-  if (H.status != 0) {
-    if (tid == 0) put_stats(A, m, H.status, H.E, 0, 0, 0, 0, 0, 0);
+  if (st2 != 0) {
+    if (tid == 0) put_stats(A, m, st2, E, 0, 0, 0, 0, 0, 0);
     return;
   }
 
@@ -1173,8 +1189,10 @@ void k_fused(FusedArgs A) {
   }
   __syncthreads();
   auto cc_size = [&](uint32_t r) { return (int)((ccsz[r >> 1] >> (16 * (r & 1))) & 0xFFFF); };
+  int nodes, cc_max;
   {
-    // nodes and roots packed in one 64-bit sum, the largest size in one max
+    // nodes and roots packed in one 64-bit sum, the largest size in one max; every thread
+    // reads the per-wave partials (no thread-0 section and second barrier)
     int64_t nr = 0;
     int mx = 0;
     for (int i = tid; i < n; i += FWG) {
@@ -1183,22 +1201,22 @@ void k_fused(FusedArgs A) {
         if (S.parent[i] == (uint32_t)i) { nr += 1; mx = max(mx, cc_size(i)); }
       }
     }
+    nr = wave_incl_scan(nr, [](int64_t a, int64_t b) { return a + b; });
+    mx = wave_incl_scan(mx, [](int a, int b) { return max(a, b); });
+    if ((tid & 63) == 63) { H.red64[tid >> 6] = nr; H.redi[tid >> 6] = mx; }
+    __syncthreads();
+    int64_t t = 0;
+    int m2 = 0;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      nr += __shfl_xor(nr, o, 64);
-      mx = max(mx, __shfl_xor(mx, o, 64));
-    }
-    if ((tid & 63) == 0) { H.red64[tid >> 6] = nr; H.redi[tid >> 6] = mx; }
-    __syncthreads();
-    if (tid == 0) {
-      int64_t t = 0;
-      int m2 = 0;
-      for (int w = 0; w < FNW; ++w) { t += H.red64[w]; m2 = max(m2, H.redi[w]); }
-      H.nodes = (int)(t >> 32); H.cc_cnt = (int)(t & 0xFFFFFFFF); H.cc_max = m2;
-    }
-    __syncthreads();
+    for (int w = 0; w < FNW; ++w) { t += H.red64[w]; m2 = max(m2, H.redi[w]); }
+    nodes = (int)(t >> 32);
+    cc_max = m2;
+    if (tid == 0) { H.nodes = nodes; H.cc_cnt = (int)(t & 0xFFFFFFFF); H.cc_max = cc_max; }
   }
+  // (no barrier: the P4 passes below start with their own before touching the reduction
+  // slots, and no array read here is written before it)
   const bool get_cc = (A.flags & 1) != 0;
+  int target = -1;
   if (get_cc) {
     // largest CC; ties -> the component whose first edge comes first in the enumeration
     uint64_t best = ~0ULL;
@@ -1206,7 +1224,7 @@ void k_fused(FusedArgs A) {
       const int e0 = S.fwd[i], e1 = S.fwd[i + 1];
       if (e0 == e1) continue;
       const uint32_t r = S.parent[i];
-      if (cc_size(r) != H.cc_max) continue;
+      if (cc_size(r) != cc_max) continue;
       // the box's first edge in enumeration order: lowest target picker (the first segment
       // of the position-sorted list), smallest file index inside it
       const int pi = picker_of<K>(c.pp, i);
@@ -1220,18 +1238,22 @@ void k_fused(FusedArgs A) {
                            ((uint64_t)(hmin - picker_begin<K>(c.pb, ph)) << 16) | r;
       best = key < best ? key : best;
     }
-    best = block_min_u64<FWG>(best, H.redu);
-    if (tid == 0) H.target = (int)(best & 0xFFFF);
+    // redu is not aliased by red64/redi (only P0's red4 covers it): one barrier
+    best = wave_incl_scan(best, [](uint64_t a, uint64_t b) { return a < b ? a : b; });
+    if ((tid & 63) == 63) H.redu[tid >> 6] = best;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < FNW; ++w) best = H.redu[w] < best ? H.redu[w] : best;
+    target = (int)(best & 0xFFFF);
+    if (tid == 0) H.target = target;
   }
-  __syncthreads();
 
   STOP_AFTER(3);
   STAMP(7);   // CC stats
   // ---- P4: k-cliques (level-synchronous BFS into the queue region; per-root DFS counts as the
   // fallback when a level does not fit), vertex marking, output reservation
-  c.set_order = 2 * K < H.nodes;
+  c.set_order = 2 * K < nodes;
   const int n0 = c.pp[1];   // roots: picker-0 positions
-  const int target = H.target;
   // queue region: after the E used entries of dst through the cell starts (contiguous: dst
   // immediately precedes the cell starts in the layout)
   const int qoff = (L.off_dst + 2 * H.E + 15) & ~15;
@@ -1292,7 +1314,7 @@ void k_fused(FusedArgs A) {
       S.cnt[r] = cntr;
     }
     __syncthreads();
-    C = block_scan_array<FWG>(S.cnt, n0, H.red64);
+    C = block_scan_dpp<FWG>(S.cnt, n0, H.red64);
     if (tid == 0) S.cnt[n0] = (uint32_t)C;
     c.cq_cap = qbytes / (2 * K + 2);
     c.cq_ord = S.cbuf + (size_t)c.cq_cap * K;
@@ -1338,7 +1360,7 @@ void k_fused(FusedArgs A) {
       S.vrank[t] = (uint16_t)((atomicAdd(&bw[q >> 1], 1u << sh) >> sh) & 0xFFFFu);
     }
     __syncthreads();
-    const int64_t V = block_scan_u16<FWG>(bcnt, n, H.red64);
+    const int64_t V = block_scan_dpp<FWG>(bcnt, n, H.red64);
     if (tid == 0) { H.V = (int)V; bcnt[n] = (uint16_t)V; }
     for (int t = tid; t < n; t += FWG) {
       if (S.flags[t] != 3) continue;
