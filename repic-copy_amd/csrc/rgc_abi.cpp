@@ -85,7 +85,6 @@ struct Buf {
 // API over-reports 3 up to 54613 B, so it is not used).
 constexpr int LDS_BLOCK = 1280;
 constexpr int LDS_BLOCKS = 128;
-constexpr int FUSED_WG = 512;
 // Micrographs above this many boxes go straight to the large-micrograph route.  Above 2048
 // boxes the fused layout uses 2 n grid cells and u16 parents (29 B per box + 2 B per edge),
 // so a 4096-box micrograph (C3: ~4k boxes, ~15k edges) runs in one workgroup per CU with room
@@ -97,32 +96,48 @@ constexpr size_t CUR_BYTES = 32;
 static int lds_blocks(int bytes) { return (bytes + LDS_BLOCK - 1) / LDS_BLOCK; }
 
 // One fused launch configuration: micrographs of <= nmax boxes, forward-edge capacity ecap,
-// dynamic LDS bytes, coordinate width.
+// dynamic LDS bytes, coordinate width, workgroup size.
 struct FusedPlan {
   int nmax = 0, ecap = 0, lds = 0, wg = 0;   // wg: workgroups per CU
+  int nt = 512;                              // threads per workgroup
   bool wide = false;
 };
 
-// Workgroups per CU the kernel's VGPRs allow (8 waves per workgroup, 4 SIMDs, 512 VGPRs).
-static int vgpr_wg_cap(int k, bool wide) {
-  static int cache[2][MAX_K + 1] = {};
-  int& v = cache[wide][k];
+// Workgroups per CU the VGPRs of the nt-thread kernel allow (nt / 64 waves per workgroup over
+// 4 SIMDs of 512 VGPRs, at most 8 waves per SIMD).
+static int vgpr_wg_cap(int k, bool wide, int nt) {
+  static int cache[2][MAX_K + 1][3] = {};
+  int& v = cache[wide][k][nt == 512 ? 0 : (nt == 768 ? 1 : 2)];
   if (!v) {
-    const int r = fused_vgprs(k, wide);
-    const int waves = r > 0 ? std::min(8, 512 / (((r + 7) / 8) * 8)) : 1;
-    v = std::max(1, waves * 4 / (FUSED_WG / 64));
+    const int r = fused_vgprs(k, wide, nt);
+    const int waves = r > 0 ? std::min(8, 512 / (((r + 7) / 8) * 8)) : 0;
+    v = 1 + waves * 4 / (nt / 64);   // stored + 1 (0 = not computed)
   }
-  return v;
+  return v - 1;
 }
 
 // The most workgroups per CU that LDS (with ecap >= nmax) and VGPRs allow, then the largest
-// edge capacity at that occupancy (free LDS up to the next allocation boundary).
-// max_wg = 1: the whole 160 KiB (largest ecap).
+// edge capacity at that occupancy (free LDS up to the next allocation boundary).  Among the
+// compiled workgroup sizes the one with the most resident waves per CU wins (ties: the
+// smallest): where LDS admits only one or two workgroups per CU, 768 / 1024 threads put the
+// idle SIMD slots to work.  max_wg = 1: the whole 160 KiB (largest ecap).
+// RGC_DIAG_NT (experiments only) forces one workgroup size when it is compiled for k.
 static bool plan_fused(int k, bool wide, int nmax, int max_wg, FusedPlan* p) {
   const int base = fused_lds_bytes(nmax, 0, wide);
   const int need = lds_blocks(fused_lds_bytes(nmax, nmax, wide));
   if (need > LDS_BLOCKS) return false;
-  const int w = std::min(std::min(max_wg, vgpr_wg_cap(k, wide)), LDS_BLOCKS / need);
+  static const int diag_nt = [] {
+    const char* e = getenv("RGC_DIAG_NT");
+    return e ? atoi(e) : 0;
+  }();
+  int w = 0, nt = 512, best_waves = 0;
+  for (int cand : {512, 768, 1024}) {
+    if (!fused_nt_ok(k, cand) || (diag_nt && fused_nt_ok(k, diag_nt) && cand != diag_nt)) continue;
+    const int wc = std::min(std::min(max_wg, vgpr_wg_cap(k, wide, cand)), LDS_BLOCKS / need);
+    if (wc < 1) continue;
+    if (wc * cand / 64 > best_waves) { best_waves = wc * cand / 64; w = wc; nt = cand; }
+  }
+  if (w < 1) return false;
   const int budget = (LDS_BLOCKS / w) * LDS_BLOCK;
   int ecap = std::min(65535, (budget - base) / 2);
   while (ecap > nmax && fused_lds_bytes(nmax, ecap, wide) > budget) ecap -= 8;
@@ -130,6 +145,7 @@ static bool plan_fused(int k, bool wide, int nmax, int max_wg, FusedPlan* p) {
   p->ecap = ecap;
   p->wide = wide;
   p->wg = w;
+  p->nt = nt;
   p->lds = fused_lds_bytes(nmax, ecap, wide);
   return p->lds <= budget;
 }
@@ -615,7 +631,8 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   }
   const bool all0 = !no_fused && n_mg > 0 && nmaxb <= FUSED_MAX_BOXES &&
                     plan_of(0, fused_class(nmaxb)).nmax &&
-                    plan_of(0, fused_class(nmin)).wg == plan_of(0, fused_class(nmaxb)).wg;
+                    plan_of(0, fused_class(nmin)).wg == plan_of(0, fused_class(nmaxb)).wg &&
+                    plan_of(0, fused_class(nmin)).nt == plan_of(0, fused_class(nmaxb)).nt;
   if (!all0) {
     todo0.reserve(n_mg);
     for (int m = 0; m < n_mg; ++m) {
@@ -703,11 +720,13 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
           A.stamps = D<unsigned long long>(c, D_STAMPS) + (size_t)(ml_off + starts[q]) * 16;
 #endif
           TRY(mark(c, "k_fused"));
-          const int le = launch_fused(s, single ? n_mg : (int)lists[q].size(), pl.lds, A, wide);
+          const int le = launch_fused(s, single ? n_mg : (int)lists[q].size(), pl.lds, A, wide,
+                                      pl.nt);
           if (le != 0)
             return fail(std::string("fused kernel launch failed (k=") + std::to_string(k) +
                         (wide ? ", f64" : ", f32") + " layout, nmax " + std::to_string(pl.nmax) +
-                        ", lds " + std::to_string(pl.lds) + "): " +
+                        ", lds " + std::to_string(pl.lds) + ", " +
+                        std::to_string(pl.nt) + " threads): " +
                         (le > 0 ? hipGetErrorString((hipError_t)le) : "unsupported k"));
         }
         TRY(mark(c, "d2h_stats"));

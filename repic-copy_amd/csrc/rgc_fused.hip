@@ -27,8 +27,11 @@
 
 namespace rgc {
 
-constexpr int FWG = 512;            // fused-kernel workgroup: 8 waves per micrograph
+constexpr int FWG = 512;            // default fused-kernel workgroup: 8 waves per micrograph
 constexpr int FNW = FWG / 64;
+constexpr int MAXW = 16;            // reduction slots: up to 1024-thread workgroups
+// Workgroup sizes compiled: 512 for every k; 768 / 1024 threads (12 / 16 waves) for k <= 5,
+// launched when LDS allows few workgroups per CU but VGPRs allow more waves (rgc_abi.cpp).
 constexpr int RB = 2;               // boxes per thread kept in registers from P0 to P1
 
 struct FusedHdr {
@@ -36,12 +39,12 @@ struct FusedHdr {
   // starts behind a barrier)
   union {
     struct {
-      double redd[FNW];
-      int64_t red64[FNW];
-      uint64_t redu[FNW];
-      int redi[FNW];
+      double redd[MAXW];
+      int64_t red64[MAXW];
+      uint64_t redu[MAXW];
+      int redi[MAXW];
     };
-    double red4[4][FNW];
+    double red4[4][MAXW];
   };
   double minx, miny, cell, inv_cell;
   double xbs;       // P5 x-bucket scale: bucket(x) = min(trunc((x - minx) * xbs), n - 1)
@@ -524,7 +527,7 @@ struct BfsOut {
 // then, so first segments come from a binary search for the next picker's first position and
 // a root is valid iff it was marked as a clique vertex in P4 (it has a clique, which lies in
 // the --get_cc target component); vertices are already marked.
-template <int K, int D>
+template <int K, int D, int NT>
 struct BfsLevel {
   // prefix members of entry e of level D (D members, compile-time indices only)
   __device__ __forceinline__ static void prefix(const char* q, const int (&lvl)[K + 1],
@@ -557,7 +560,7 @@ struct BfsLevel {
     if (nD > 65535 || tb < lvl[D] + 4 * (int)nD) { out.C = -1; return out; }
     uint32_t* MK = reinterpret_cast<uint32_t*>(q + tb);
     uint32_t* CN = MK + nD;
-    for (int e = tid; e < nD; e += FWG) {
+    for (int e = tid; e < nD; e += NT) {
       int mm[K];
       prefix(q, lvl, (uint32_t)e, mm);
       const int m = mm[D - 1];
@@ -576,11 +579,11 @@ struct BfsLevel {
       CN[e] = cnt;
     }
     __syncthreads();
-    const int64_t nN = block_scan_dpp<FWG>(CN, (int)nD, H.red64);
+    const int64_t nN = block_scan_dpp<NT>(CN, (int)nD, H.red64);
     constexpr bool last = D + 1 == K;
     const int nb = (lvl[D] + 4 * (int)nD + 3) & ~3;   // next level starts here
     if (nN > 65535 || nN * (last ? 6 : 4) > tb - nb) { out.C = -1; return out; }
-    for (int e = tid; e < nD; e += FWG) {
+    for (int e = tid; e < nD; e += NT) {
       int mm[K];
       prefix(q, lvl, (uint32_t)e, mm);
       const int m = mm[D - 1];
@@ -614,7 +617,7 @@ struct BfsLevel {
     __syncthreads();
     lvl[D + 1] = nb;
     if constexpr (D + 1 < K) {
-      return BfsLevel<K, D + 1>::template run<REWALK>(S, H, q, qbytes, out, nN, tid, pp);
+      return BfsLevel<K, D + 1, NT>::template run<REWALK>(S, H, q, qbytes, out, nN, tid, pp);
     } else {
       out.C = nN;
       return out;
@@ -625,7 +628,7 @@ struct BfsLevel {
 // Cliques of the roots [r0, r1) (picker-0 positions).  Returns C = -1 when a level does not
 // fit the queue region; the caller then retries with fewer roots (root chunks, P4) and falls
 // back to the per-root DFS only when a single root does not fit.
-template <int K, bool REWALK>
+template <int K, bool REWALK, int NT>
 __device__ __forceinline__ BfsOut<K> bfs_cliques(const FShared& S, FusedHdr& H, char* q,
                                                  int qbytes, int r0, int r1, bool get_cc,
                                                  uint32_t target, int tid,
@@ -645,15 +648,15 @@ __device__ __forceinline__ BfsOut<K> bfs_cliques(const FShared& S, FusedHdr& H, 
   };
   // level 1 -> 2: every root's first segment (picker-1 neighbours), no checks needed
   uint32_t* cnt = S.cnt;
-  for (int i = tid; i < nr; i += FWG) {
+  for (int i = tid; i < nr; i += NT) {
     const int r = r0 + i;
     cnt[i] = root_ok(r) ? (uint32_t)(seg_end(r) - S.fwd[r]) : 0u;
   }
   __syncthreads();
-  const int64_t n2 = block_scan_dpp<FWG>(cnt, nr, H.red64);
+  const int64_t n2 = block_scan_dpp<NT>(cnt, nr, H.red64);
   constexpr bool last = K == 2;
   if (n2 > 65535 || n2 * (last ? 6 : 4) > qbytes) return out;
-  for (int i = tid; i < nr; i += FWG) {
+  for (int i = tid; i < nr; i += NT) {
     const int r = r0 + i;
     if (!root_ok(r)) continue;
     uint32_t o = cnt[i];
@@ -673,7 +676,7 @@ __device__ __forceinline__ BfsOut<K> bfs_cliques(const FShared& S, FusedHdr& H, 
   __syncthreads();
   out.lvl[2] = 0;
   if constexpr (K > 2) {
-    return BfsLevel<K, 2>::template run<REWALK>(S, H, q, qbytes, out, n2, tid, pp);
+    return BfsLevel<K, 2, NT>::template run<REWALK>(S, H, q, qbytes, out, n2, tid, pp);
   } else {
     out.C = n2;
     return out;
@@ -849,14 +852,18 @@ __device__ __forceinline__ void put_stats(const FusedArgs& A, int m, int status,
 // waves per SIMD = 4 workgroups per CU, which the f32-coordinate LDS layout also allows; larger
 // K keep the compiler's choice (their VGPRs, not LDS, bound the occupancy).
 #ifdef RGC_X_NOWPE   // timing experiment: compiler's own register budget
-constexpr int fused_waves_per_eu(int) { return 1; }
+constexpr int fused_waves_per_eu(int, int) { return 1; }
 #else
-constexpr int fused_waves_per_eu(int k) { return k <= 3 ? 8 : 1; }
+constexpr int fused_waves_per_eu(int k, int nt) {
+  return nt == 1024 ? 4 : (nt == 768 ? 6 : (k <= 3 ? 8 : 1));
+}
 #endif
 
-template <int K, bool W>
-__global__ __launch_bounds__(FWG) __attribute__((amdgpu_waves_per_eu(fused_waves_per_eu(K))))
+template <int K, bool W, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(fused_waves_per_eu(K, NT))))
 void k_fused(FusedArgs A) {
+  constexpr int FWG = NT;   // (shadows the default) threads of this instance
+  constexpr int FNW = NT / 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   FusedHdr& H = *reinterpret_cast<FusedHdr*>(smem);
   const FusedLayout L = fused_layout(A.nmax, A.ecap, W);
@@ -1277,7 +1284,7 @@ void k_fused(FusedArgs A) {
     if (tid == 0) { chtab[0] = 0; chtab[1] = 0; }
     while (ok && r0 < n0) {
       len = min(len, n0 - r0);
-      bo = bfs_cliques<K, false>(S, H, q, qbytes, r0, r0 + len, get_cc, (uint32_t)target, tid,
+      bo = bfs_cliques<K, false, NT>(S, H, q, qbytes, r0, r0 + len, get_cc, (uint32_t)target, tid,
                                  c.pp);
       if (bo.C < 0) {
         ok = K >= 4 && len > 1;
@@ -1422,7 +1429,7 @@ void k_fused(FusedArgs A) {
         c1 = ufl((int)chtab[2 * ch + 3]);
         if constexpr (K >= 4) {
           if (ci > 0)
-            cur = bfs_cliques<K, true>(S, H, q, qbytes, ufl((int)chtab[2 * ch]),
+            cur = bfs_cliques<K, true, NT>(S, H, q, qbytes, ufl((int)chtab[2 * ch]),
                                        ufl((int)chtab[2 * ch + 2]), get_cc, (uint32_t)target,
                                        tid, c.pp);
         }
@@ -1445,7 +1452,7 @@ void k_fused(FusedArgs A) {
       // members of chunk slot sl: BFS tree walk, or the re-walk buffer
       auto clique_members = [&](int sl, int (&mem)[K]) {
         if (bfs_ok) {
-          BfsLevel<K, K>::prefix(q, cur.lvl, (uint32_t)sl, mem);
+          BfsLevel<K, K, NT>::prefix(q, cur.lvl, (uint32_t)sl, mem);
         } else {
           const uint16_t* sb = S.cbuf + sl * K;
 #pragma unroll
@@ -1480,31 +1487,57 @@ void k_fused(FusedArgs A) {
     put_stats(A, m, H.status, H.E, H.nodes, H.cc_cnt, H.cc_max, H.V, H.base, H.C);
 }
 
-template <int K, bool W>
+template <int K, bool W, int NT>
 static int launch_fused_t(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArgs& A) {
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused<K, W>),
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused<K, W, NT>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((k_fused<K, W>), dim3(n_blocks), dim3(FWG), lds_bytes, stream, A);
+  hipLaunchKernelGGL((k_fused<K, W, NT>), dim3(n_blocks), dim3(NT), lds_bytes, stream, A);
   return (int)hipGetLastError();
 }
 
-template <int K, bool W>
+template <int K, bool W, int NT>
 static int fused_vgprs_t() {
   hipFuncAttributes at;
-  if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&k_fused<K, W>)) != hipSuccess)
+  if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&k_fused<K, W, NT>)) != hipSuccess)
     return -1;
   return at.numRegs;
 }
 
-int fused_vgprs(int k, bool wide) {
+// workgroup sizes compiled for k (fused_nt_ok) and their dispatch
+bool fused_nt_ok(int k, int nt) {
+  if (k < 2 || k > 8) return false;
+  return nt == 512 || ((nt == 768 || nt == 1024) && k <= 5);
+}
+
+template <int K, bool W>
+static int fused_vgprs_k(int nt) {
+  if constexpr (K <= 5) {
+    if (nt == 768) return fused_vgprs_t<K, W, 768>();
+    if (nt == 1024) return fused_vgprs_t<K, W, 1024>();
+  }
+  return nt == 512 ? fused_vgprs_t<K, W, 512>() : -1;
+}
+
+template <int K, bool W>
+static int launch_fused_k(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArgs& A,
+                          int nt) {
+  if constexpr (K <= 5) {
+    if (nt == 768) return launch_fused_t<K, W, 768>(stream, n_blocks, lds_bytes, A);
+    if (nt == 1024) return launch_fused_t<K, W, 1024>(stream, n_blocks, lds_bytes, A);
+  }
+  return nt == 512 ? launch_fused_t<K, W, 512>(stream, n_blocks, lds_bytes, A) : -1;
+}
+
+int fused_vgprs(int k, bool wide, int nt) {
+  if (!fused_nt_ok(k, nt)) return -1;
   switch (k) {
 #define RGC_VG_CASE(KK) \
-  case KK: return wide ? fused_vgprs_t<KK, true>() : fused_vgprs_t<KK, false>();
+  case KK: return wide ? fused_vgprs_k<KK, true>(nt) : fused_vgprs_k<KK, false>(nt);
     RGC_VG_CASE(2) RGC_VG_CASE(3) RGC_VG_CASE(4) RGC_VG_CASE(5) RGC_VG_CASE(6) RGC_VG_CASE(7)
     RGC_VG_CASE(8)
 #undef RGC_VG_CASE
@@ -1513,13 +1546,15 @@ int fused_vgprs(int k, bool wide) {
   }
 }
 
-int launch_fused(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArgs& A, bool wide) {
+int launch_fused(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArgs& A, bool wide,
+                 int nt) {
   if (n_blocks <= 0) return 0;
+  if (!fused_nt_ok(A.k, nt)) return -1;
   switch (A.k) {
-#define RGC_FUSED_CASE(KK)                                                          \
-  case KK:                                                                          \
-    return wide ? launch_fused_t<KK, true>(stream, n_blocks, lds_bytes, A)          \
-                : launch_fused_t<KK, false>(stream, n_blocks, lds_bytes, A);
+#define RGC_FUSED_CASE(KK)                                                            \
+  case KK:                                                                            \
+    return wide ? launch_fused_k<KK, true>(stream, n_blocks, lds_bytes, A, nt)        \
+                : launch_fused_k<KK, false>(stream, n_blocks, lds_bytes, A, nt);
     RGC_FUSED_CASE(2)
     RGC_FUSED_CASE(3)
     RGC_FUSED_CASE(4)

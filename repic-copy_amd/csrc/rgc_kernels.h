@@ -92,8 +92,10 @@ struct FusedArgs {
 };
 
 int fused_lds_bytes(int nmax, int ecap, bool wide);
-int fused_vgprs(int k, bool wide);
-int launch_fused(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArgs& A, bool wide);
+int fused_vgprs(int k, bool wide, int nt);
+bool fused_nt_ok(int k, int nt);
+int launch_fused(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArgs& A, bool wide,
+                 int nt);
 void launch_gather(hipStream_t stream, int n_sub, int k, const int32_t* sub_mg,
                    const int32_t* box_off, const int32_t* sub_box_off, const double* x,
                    const double* y, const double* s, double* ox, double* oy, double* os,
