@@ -169,11 +169,12 @@ PYS_FN uint32_t set_order_packed(const uint64_t (&h)[N]) {
   for (int t = 0; t < N; ++t) {
     slot[t] = pk_probe(lo, hi, mask, h[t]);
     pk_set(lo, hi, slot[t], t);
-    if (t == 4) {   // fill 5: 5 * 5 >= 7 * 3 -> set_table_resize to 32 slots
+    if (N > 4 && t == 4) {   // fill 5: 5 * 5 >= 7 * 3 -> set_table_resize to 32 slots
+      constexpr int R = N > 4 ? 5 : N;   // N <= 4 never resizes (keeps the indices in range)
       uint64_t ks[5], kh[5];
       int kt[5];
 #pragma unroll
-      for (int i = 0; i < 5; ++i) { ks[i] = slot[i]; kh[i] = h[i]; kt[i] = i; }
+      for (int i = 0; i < R; ++i) { ks[i] = slot[i]; kh[i] = h[i]; kt[i] = i; }
 #pragma unroll
       for (int i = 0; i < 5; ++i)
 #pragma unroll

@@ -27,8 +27,6 @@
 
 namespace rgc {
 
-constexpr int FWG = 512;            // default fused-kernel workgroup: 8 waves per micrograph
-constexpr int FNW = FWG / 64;
 constexpr int MAXW = 16;            // reduction slots: up to 1024-thread workgroups
 // Workgroup sizes compiled: 512 for every k; 768 / 1024 threads (12 / 16 waves) for k <= 5,
 // launched when LDS allows few workgroups per CU but VGPRs allow more waves (rgc_abi.cpp).
@@ -862,7 +860,7 @@ constexpr int fused_waves_per_eu(int k, int nt) {
 template <int K, bool W, int NT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(fused_waves_per_eu(K, NT))))
 void k_fused(FusedArgs A) {
-  constexpr int FWG = NT;   // (shadows the default) threads of this instance
+  constexpr int FWG = NT;   // threads of this instance
   constexpr int FNW = NT / 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   FusedHdr& H = *reinterpret_cast<FusedHdr*>(smem);
