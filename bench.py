@@ -64,9 +64,10 @@ def pipeline_bytes(N, E, C, k):
     return 28 * N + 32 * E + C * (20 * k + 12)
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, config):
     """HBM bytes per launch of ``kernel`` from the newest profiles/*_traffic.json written by
-    tools/pmc_traffic.py for THIS library build (sha256 must match), else None."""
+    tools/pmc_traffic.py for THIS library build (sha256 must match) on THIS workload
+    (config; files without one were C2 runs), else None."""
     import glob
     import hashlib
     from repic_amd import _lib
@@ -76,7 +77,8 @@ def pmc_traffic(kernel):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if d.get("lib_sha256") == sha and kernel in d.get("kernels", {}):
+        if (d.get("lib_sha256") == sha and d.get("config", "C2") == config
+                and kernel in d.get("kernels", {})):
             return d["kernels"][kernel]["traffic"], os.path.basename(f)
     return None, None
 
@@ -320,7 +322,7 @@ def main():
         dom_bytes = pipe
         dom_ms = dev_ms
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic("k_fused" if dom == "k_fused" else dom)
+    traffic, traffic_src = pmc_traffic("k_fused" if dom == "k_fused" else dom, args.config)
     out = {
         "metric": "micrographs/sec (get_cliques, whole node) at 1/2/4/8 MI355X; % HBM roofline",
         "value": value, "unit": "micrographs/s", "n_gpus": world, "steps": steps,

@@ -44,6 +44,7 @@ struct FusedHdr {
     };
     double red4[4][MAXW];
   };
+  int nonint[MAXW];   // P0: per wave, some finite coordinate is not an integer in (-2^23, 2^23)
   double minx, miny, cell, inv_cell;
   double xbs;       // P5 x-bucket scale: bucket(x) = min(trunc((x - minx) * xbs), n - 1)
   float inv_gy;
@@ -794,6 +795,34 @@ __device__ __forceinline__ int pairs_count(const Stencil& st, const FShared& S, 
   return cnt;
 }
 
+// P2 count on integer coordinates (f32 layout, see P2): exact f32 overlaps, I > floor(6B^2/13)
+template <int K>
+__device__ __forceinline__ int pairs_count_int(const Stencil& st, const FShared& S,
+                                               const GridU& H, float Bf, float Tf,
+                                               uint32_t* mask_out) {
+  uint32_t mask = 0;
+  int cnt = 0, kk = 0;
+  const float ax = (float)st.a.x, ay = (float)st.a.y;
+  for (int q = st.p + 1; q < K; ++q) {
+#pragma unroll
+    for (int d = -1; d <= 1; ++d) {
+      int lo, hi;
+      stencil_range(st, S, H, q, d, lo, hi);
+      for (int t = lo; t < hi; ++t, ++kk) {
+        const float2 bf = reinterpret_cast<const float2*>(S.sxy)[t];
+        const float xo = fmaxf(Bf - fabsf(ax - bf.x), 0.0f);
+        const float yo = fmaxf(Bf - fabsf(ay - bf.y), 0.0f);
+        if (xo * yo > Tf) {
+          ++cnt;
+          mask |= (kk < 32) ? (1u << kk) : 0u;
+        }
+      }
+    }
+  }
+  *mask_out = mask;
+  return cnt;
+}
+
 // P2 fill: write the box's forward targets (positions) at d[0..cnt) from the count's bitmask
 // (re-testing candidates past the 32nd).  Grids are visited in picker order and each grid's
 // column ranges in key order, so the list comes out sorted.
@@ -943,10 +972,12 @@ void k_fused(FusedArgs A) {
   };
   double mnx = INFINITY, mny = INFINITY, mxx = -INFINITY, mxy = -INFINITY;
   bool inexact = false;   // a coordinate not exactly representable as f32 (NaN excepted)
+  bool nonint = false;    // a finite box with a coordinate off the integer grid (-2^23, 2^23)
   each_box([&](int, double xv, double yv) {
     if (isfinite(xv) && isfinite(yv)) {
       mnx = fmin(mnx, xv); mxx = fmax(mxx, xv);
       mny = fmin(mny, yv); mxy = fmax(mxy, yv);
+      nonint |= xv != rint(xv) || yv != rint(yv) || fabs(xv) >= 0x1p23 || fabs(yv) >= 0x1p23;
     }
     if (!W) inexact |= ((double)(float)xv != xv && xv == xv) || ((double)(float)yv != yv && yv == yv);
   });
@@ -973,6 +1004,8 @@ void k_fused(FusedArgs A) {
     if ((tid & 63) == 63)
 #pragma unroll
       for (int r = 0; r < 4; ++r) H.red4[r][tid >> 6] = v[r];
+    const bool wn = __any(nonint);
+    if ((tid & 63) == 0) H.nonint[tid >> 6] = wn ? 1 : 0;
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -1090,6 +1123,20 @@ void k_fused(FusedArgs A) {
   // band moves the quotient by >= 1.1e-12 relative), so the decision is the reference's.
   const double t_star = 0.6 * B * B / 1.3;
   const double i_lo = t_star * (1.0 - 0x1p-40), i_hi = t_star * (1.0 + 0x1p-40);
+  // integer coordinates (|v| < 2^23) and an integer 1 <= B <= 4095: the overlaps B - |dx| and
+  // their product (< 2^24) are exact in f32 and JI > 0.3 <=> I > floor(6 B^2 / 13) (at
+  // I = 6 B^2 / 13 the reference's quotient rounds to 0.3 itself, not above it), so the count
+  // pass decides every candidate with six f32 operations (edge_test_int)
+  bool intp = false;
+  int ti = 0;
+  if (!W && B >= 1.0 && B <= 4095.0 && B == floor(B)) {
+    int nw = 0;
+#pragma unroll
+    for (int w = 0; w < FNW; ++w) nw |= H.nonint[w];
+    intp = nw == 0;
+    const int bi = (int)B;
+    ti = (6 * bi * bi) / 13;
+  }
   // thread per box (sorted position): lanes of a wave hold neighbouring boxes of one picker,
   // so their stencils overlap (similar trip counts, broadcast LDS reads), and the waves of
   // picker K-1 have nothing to do.  cnt[] (dead until P3) keeps
@@ -1104,7 +1151,10 @@ void k_fused(FusedArgs A) {
     Stencil st;
     stencil_setup<K, W>(st, ts, S, G);
     uint32_t mask;
-    S.fwd[ts] = (uint16_t)pairs_count<K, W>(st, S, G, B, two_b2, i_lo, i_hi, &mask);
+    int ec;
+    if (!W && intp) ec = pairs_count_int<K>(st, S, G, (float)B, (float)ti, &mask);
+    else ec = pairs_count<K, W>(st, S, G, B, two_b2, i_lo, i_hi, &mask);
+    S.fwd[ts] = (uint16_t)ec;
     S.cnt[ts] = mask;
   }
   __syncthreads();

@@ -6,7 +6,9 @@ reads exactly 1/2 of a wide (16 B/lane) coalesced streaming read on gfx950; our 
 4-8 B per lane in gathers, a width the guide leaves uncalibrated, so the fetch side is
 reported raw (x1024) and flagged, not doubled.
 
-  python tools/pmc_traffic.py FETCH.csv WRITE.csv LIB.so OUT.json
+  python tools/pmc_traffic.py FETCH.csv WRITE.csv LIB.so OUT.json [CONFIG]
+
+CONFIG (default C2) is recorded so bench.py only quotes traffic measured on its own workload.
 """
 import csv
 import hashlib
@@ -41,10 +43,10 @@ def per_kernel(path, counter):
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 
-def main(fetch, write, lib, out):
+def main(fetch, write, lib, out, config="C2"):
     f, w = per_kernel(fetch, "FETCH_SIZE"), per_kernel(write, "WRITE_SIZE")
     sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()
-    res = {"lib_sha256": sha, "unit": "bytes per launch",
+    res = {"lib_sha256": sha, "config": config, "unit": "bytes per launch",
            "note": "FETCH_SIZE*1024 (raw, uncalibrated width) + WRITE_SIZE*1024",
            "kernels": {k: {"fetch": f.get(k), "write": w.get(k),
                            "traffic": (f.get(k) or 0.0) + (w.get(k) or 0.0)}
@@ -55,4 +57,4 @@ def main(fetch, write, lib, out):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:5])
+    main(*sys.argv[1:6])
