@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RGC_ABI_VERSION 2
+#define RGC_ABI_VERSION 3
 
 /* flags for rgc_batch_in.flags */
 #define RGC_F_GET_CC         1u  /* --get_cc   (get_cliques.py:151-156) */
@@ -114,6 +114,16 @@ int rgc_device_count(int* n);
 int rgc_ctx_create(int device, void* hip_stream, rgc_ctx** out);
 void rgc_ctx_destroy(rgc_ctx* ctx);
 int rgc_run(rgc_ctx* ctx, const rgc_batch_in* in, rgc_batch_out* out);
+/* Asynchronous rgc_run (ABI 3), one run in flight per context: rgc_submit enqueues the batch
+ * on the context's stream and returns; rgc_wait blocks until it is done and fills *out exactly
+ * as rgc_run would.  Host and device arrays of the batch must stay valid until rgc_wait.  A
+ * batch that takes the single fused launch (HBM-resident inputs and offsets, RGC_F_DEVICE_INPUTS
+ * | RGC_F_DEVICE_META, device outputs) runs while the caller continues, so with two contexts
+ * on one stream the host prepares and launches batch i+1 while the device runs batch i; any
+ * other batch (or one whose micrographs need a second pass) runs through rgc_run's general
+ * path.  Outputs stay valid until the next submit/run on the same context. */
+int rgc_submit(rgc_ctx* ctx, const rgc_batch_in* in);
+int rgc_wait(rgc_ctx* ctx, rgc_batch_out* out);
 /* Per-kernel device milliseconds of the last rgc_run with RGC_F_TIMING; returns the count. */
 int rgc_kernel_times(rgc_ctx* ctx, int max_n, float* ms, const char** names);
 

@@ -194,6 +194,13 @@ struct rgc_ctx {
   void* cursor_zeroed = nullptr;
   hipEvent_t ev_tail = nullptr;    // timing: recorded after each fused pass's stats copy   // fused cursor already cleared on the stream for next run
   std::vector<uint64_t> stamps;   // diagnostic build only
+  // rgc_submit / rgc_wait: one run in flight per context
+  bool pend = false;       // a submitted run awaits rgc_wait
+  bool pend_fast = false;  // it is the single fused launch (else it already ran: pend_rc/out)
+  int pend_rc = 0;
+  rgc_batch_in pin{};      // the submitted batch (caller keeps its arrays alive until rgc_wait)
+  rgc_batch_out pend_out{};
+  hipEvent_t ev_sub = nullptr;   // after the submitted run's stats copy
 };
 
 static int ensure_dev(rgc_ctx* c, int id, size_t bytes, size_t keep = 0) {
@@ -931,6 +938,130 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   return 0;
 }
 
+// rgc_submit's fast path: a batch whose micrographs all take the single fused launch (pass 0,
+// one workgroup size and occupancy) with HBM-resident inputs and offsets and device outputs is
+// enqueued (kernel + stats copy + event) without waiting.  Returns 1 when enqueued, 0 when the
+// batch needs the general path (run synchronously by the caller), < 0 on error.
+static int submit_fast(rgc_ctx* c, const rgc_batch_in* in) {
+  const int n_mg = in->n_mg, k = in->k;
+  const uint32_t flags = in->flags;
+  const uint32_t need = RGC_F_DEVICE_INPUTS | RGC_F_DEVICE_META;
+  const uint32_t deny = RGC_F_HOST_OUTPUTS | RGC_F_EDGES | RGC_F_NO_FUSED;
+  if ((flags & need) != need || (flags & deny) || n_mg <= 0 || k < 2 || k > MAX_K) return 0;
+  if (in->box_size > (1LL << 26) || !in->dev_box_off || !in->dev_id_base) return 0;
+  const int64_t N = in->box_off[(int64_t)n_mg * k];
+  if (N >= (1LL << 31) - 1) return 0;
+  int64_t nmin = INT64_MAX, nmaxb = 0;
+  for (int m = 0; m < n_mg; ++m) {
+    const int64_t nm = in->box_off[(int64_t)(m + 1) * k] - in->box_off[(int64_t)m * k];
+    nmin = std::min(nmin, nm);
+    nmaxb = std::max(nmaxb, nm);
+  }
+  if (nmaxb > FUSED_MAX_BOXES) return 0;
+  const FusedPlan& pl = cached_plan(k, 0, fused_class(nmaxb));
+  const FusedPlan& p0 = cached_plan(k, 0, fused_class(nmin));
+  if (!pl.nmax || p0.wg != pl.wg || p0.nt != pl.nt) return 0;
+  const bool multi = (flags & RGC_F_MULTI_OUT) != 0;
+  const bool want_members = (flags & (RGC_F_MEMBERS | RGC_F_MULTI_OUT)) != 0;
+  hipStream_t s = c->stream;
+  c->timing = (flags & RGC_F_TIMING) != 0;
+  c->n_ev = 0;
+  c->n_edge_dump = 0;
+  const size_t cur_off = (mgout_bytes(n_mg) + 15) & ~(size_t)15;
+  TRY(ensure_host(c, H_MGOUT, cur_off + CUR_BYTES));
+  TRY(ensure_dev(c, D_MGOUT, cur_off + CUR_BYTES));
+  if (c->cap_cliques < 4096) c->cap_cliques = std::max<int64_t>(4096, N);
+  TRY(ensure_outputs(c, c->cap_cliques, 0, k, want_members, multi));
+  unsigned long long* d_cur = reinterpret_cast<unsigned long long*>(
+      static_cast<char*>(D<void>(c, D_MGOUT)) + cur_off);
+  if (c->cursor_zeroed != d_cur) HIPCHK(hipMemsetAsync(d_cur, 0, CUR_BYTES, s));
+  c->cursor_zeroed = nullptr;
+  FusedArgs A;
+  A.k = k;
+  A.flags = ((flags & RGC_F_GET_CC) ? 1 : 0) | (multi ? 2 : 0) | (want_members ? 32 : 0);
+  A.B = (double)in->box_size;
+  A.two_b2 = (double)(2 * in->box_size * in->box_size);
+  A.box_off = in->dev_box_off; A.id_base = in->dev_id_base;
+  A.x = in->x; A.y = in->y; A.score = in->score;
+  A.o = mgout_bind(D<void>(c, D_MGOUT), n_mg);
+  A.cursor = d_cur; A.cap = c->cap_cliques;
+  A.rows = D<int32_t>(c, D_ROWS); A.w = D<float>(c, D_W); A.conf = D<float>(c, D_CONF);
+  A.consensus = D<int32_t>(c, D_CONS);
+  A.members = want_members ? D<int32_t>(c, D_MEMBERS) : nullptr;
+  A.order = multi ? D<uint8_t>(c, D_ORDER) : nullptr;
+  A.stamps = nullptr;
+  A.eu = nullptr; A.ev = nullptr; A.eji = nullptr; A.ecap_out = 0;
+  A.nmax = pl.nmax; A.ecap = pl.ecap; A.mg_list = nullptr;
+#ifdef RGC_STAMPS
+  return 0;   // the diagnostic build times through rgc_run only
+#endif
+  TRY(mark(c, "k_fused"));
+  const int le = launch_fused(s, n_mg, pl.lds, A, false, pl.nt);
+  if (le != 0) return fail("fused kernel launch failed (submit): " +
+                           std::string(le > 0 ? hipGetErrorString((hipError_t)le) : "unsupported k"));
+  TRY(mark(c, "d2h_stats"));
+  HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOUT), D<void>(c, D_MGOUT), cur_off + CUR_BYTES,
+                        hipMemcpyDeviceToHost, s));
+  if (!c->ev_sub) HIPCHK(hipEventCreateWithFlags(&c->ev_sub, hipEventDisableTiming));
+  if (c->timing) {
+    if (!c->ev_tail) HIPCHK(hipEventCreate(&c->ev_tail));
+    HIPCHK(hipEventRecord(c->ev_tail, s));
+  }
+  HIPCHK(hipEventRecord(c->ev_sub, s));
+  HIPCHK(hipGetLastError());
+  return 1;
+}
+
+// completes a submit_fast run: 1 = outputs in *out; 0 = some micrograph needs another pass or
+// the outputs overflowed (the caller re-runs the batch with rgc_run's general path)
+static int wait_fast(rgc_ctx* c, rgc_batch_out* out) {
+  const rgc_batch_in* in = &c->pin;
+  const int n_mg = in->n_mg, k = in->k;
+  HIPCHK(hipEventSynchronize(c->ev_sub));
+  const size_t cur_off = (mgout_bytes(n_mg) + 15) & ~(size_t)15;
+  const MgOut ho = mgout_bind(H<void>(c, H_MGOUT), n_mg);
+  const unsigned long long* h_cur = reinterpret_cast<const unsigned long long*>(
+      static_cast<const char*>(H<void>(c, H_MGOUT)) + cur_off);
+  unsigned long long* d_cur = reinterpret_cast<unsigned long long*>(
+      static_cast<char*>(D<void>(c, D_MGOUT)) + cur_off);
+  bool again = (int64_t)h_cur[0] > c->cap_cliques;
+  for (int m = 0; m < n_mg && !again; ++m) again = ho.status[m] >= RGC_ST_DEFER;
+  if (again) return 0;
+  const bool multi = (in->flags & RGC_F_MULTI_OUT) != 0;
+  const bool want_members = (in->flags & (RGC_F_MEMBERS | RGC_F_MULTI_OUT)) != 0;
+  std::memset(out, 0, sizeof(*out));
+  out->status = ho.status;
+  out->cc_max = ho.cc_max;
+  out->cc_cnt = ho.cc_cnt;
+  out->n_nodes = ho.n_nodes;
+  out->n_vert = ho.n_vert;
+  out->n_edges_mg = ho.n_edges;
+  out->clique_base = ho.clique_base;
+  out->clique_cnt = ho.clique_cnt;
+  out->n_boxes = in->box_off[(int64_t)n_mg * k];
+  out->n_cliques = (int64_t)h_cur[0];
+  out->n_edges = (int64_t)h_cur[1];
+  out->rows = D<int32_t>(c, D_ROWS);
+  out->w = D<float>(c, D_W);
+  out->conf = D<float>(c, D_CONF);
+  out->consensus = D<int32_t>(c, D_CONS);
+  out->members = want_members ? D<int32_t>(c, D_MEMBERS) : nullptr;
+  out->order = multi ? D<uint8_t>(c, D_ORDER) : nullptr;
+  HIPCHK(hipMemsetAsync(d_cur, 0, CUR_BYTES, c->stream));   // for the next run
+  c->cursor_zeroed = d_cur;
+  if (c->timing) {
+    c->times.clear();
+    c->time_names.clear();
+    for (int i = 0; i < c->n_ev; ++i) {
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, c->events[i], i + 1 < c->n_ev ? c->events[i + 1] : c->ev_tail));
+      c->times.push_back(ms);
+      c->time_names.push_back(c->ev_names[i]);
+    }
+  }
+  return 1;
+}
+
 extern "C" {
 
 int rgc_abi_version(void) { return RGC_ABI_VERSION; }
@@ -971,6 +1102,7 @@ void rgc_ctx_destroy(rgc_ctx* c) {
     if (b.p) (void)hipHostFree(b.p);
   for (auto e : c->events) (void)hipEventDestroy(e);
   if (c->ev_tail) (void)hipEventDestroy(c->ev_tail);
+  if (c->ev_sub) (void)hipEventDestroy(c->ev_sub);
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -979,6 +1111,34 @@ int rgc_run(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   if (!c || !in || !out) return fail("null argument");
   HIPCHK(hipSetDevice(c->device));
   return run_impl(c, in, out);
+}
+
+int rgc_submit(rgc_ctx* c, const rgc_batch_in* in) {
+  if (!c || !in) return fail("null argument");
+  if (c->pend) return fail("rgc_submit: a submitted run awaits rgc_wait on this context");
+  HIPCHK(hipSetDevice(c->device));
+  c->pin = *in;
+  const int r = submit_fast(c, in);
+  if (r < 0) return r;
+  c->pend = true;
+  c->pend_fast = r == 1;
+  if (!c->pend_fast) c->pend_rc = run_impl(c, in, &c->pend_out);   // general path, now
+  return 0;
+}
+
+int rgc_wait(rgc_ctx* c, rgc_batch_out* out) {
+  if (!c || !out) return fail("null argument");
+  if (!c->pend) return fail("rgc_wait: nothing submitted on this context");
+  HIPCHK(hipSetDevice(c->device));
+  c->pend = false;
+  if (!c->pend_fast) {
+    *out = c->pend_out;
+    return c->pend_rc;
+  }
+  const int r = wait_fast(c, out);
+  if (r < 0) return r;
+  if (r == 0) return run_impl(c, &c->pin, out);   // deferrals / overflow: the general path
+  return 0;
 }
 
 int rgc_kernel_times(rgc_ctx* c, int max_n, float* ms, const char** names) {

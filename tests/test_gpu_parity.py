@@ -317,6 +317,100 @@ def test_gpu_device_resident_inputs_and_offsets():
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout + r.stderr
 
 
+def test_gpu_submit_wait_pipelined_contexts():
+    """rgc_submit / rgc_wait (ABI 3) on two contexts sharing one stream, the bench's pipelined
+    steps: every batch's outputs equal rgc_run's.  Batches cover the single-launch fast path,
+    a micrograph that needs the f64 pass (the fast path falls back at rgc_wait) and a batch
+    with a large micrograph (general path at rgc_submit).  Child process as above."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join(
+        [root, os.path.join(root, "repic-copy_amd"), here, os.environ.get("PYTHONPATH", "")]))
+    r = subprocess.run([sys.executable, "-c",
+                        "import test_gpu_parity as t; t._submit_wait_check(); print('OK')"],
+                       env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout + r.stderr
+
+
+def _d2h(ptr, n, dtype):
+    """copy n elements of a device array to numpy (HIP runtime through ctypes)"""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    out = np.empty(n, dtype=dtype)
+    if n:
+        rc = hip.hipMemcpy(ctypes.c_void_p(out.ctypes.data), ctypes.c_void_p(int(ptr)),
+                           ctypes.c_size_t(out.nbytes), ctypes.c_int(2))
+        assert rc == 0, rc
+    return out
+
+
+def _submit_wait_check():
+    import torch
+    torch.cuda.init()
+
+    from repic_amd import _lib, synth
+    from repic_amd.pipeline import Batch
+    cfg = synth.SynthConfig(**synth.CONFIGS["C2"], seed=21)
+    b1 = Batch.pack(3, 180, synth.batch(cfg, 300))
+    m2 = synth.batch(cfg, 40, start=300)
+    m2[7] = [(x + 0.25, y, s) for (x, y, s) in m2[7]]          # f64 pass: wait falls back
+    b2 = Batch.pack(3, 180, m2)
+    big = synth.SynthConfig(k=3, n_true=1800, box=60, width=4096, height=4096, keep=0.9,
+                            jit=0.08, fp=0.1, seed=22)
+    b3 = Batch.pack(3, 180, synth.batch(cfg, 20, start=400) + synth.batch(big, 1))
+    dev = torch.device("cuda", 0)
+    fl = _lib.F_MEMBERS | _lib.F_GET_CC
+    per_mg = ("status", "cc_max", "cc_cnt", "n_vert", "clique_cnt")
+    per_cl = (("rows", np.int32, 3), ("w", np.float32, 1), ("conf", np.float32, 1),
+              ("consensus", np.int32, 1), ("members", np.int32, 3))
+
+    def snap(r, on_dev):
+        d = {f: np.array(getattr(r, f)) for f in per_mg}
+        C = int(r.n_cliques)
+        for f, dt, w in per_cl:
+            v = getattr(r, f)
+            v = _d2h(v, C * w, dt) if on_dev else np.asarray(v).reshape(-1)
+            v = v.reshape(C, w) if w > 1 else v
+            d[f] = [v[int(b0):int(b0) + int(n)].copy() for b0, n in zip(r.clique_base, r.clique_cnt)]
+        return d
+
+    ref_ctx = _lib.Context(0)
+    refs, dev_in = [], []
+    for b in (b1, b2, b3):
+        refs.append(snap(ref_ctx.run(b.n_mg, 3, 180, b.box_off, b.id_base, b.x, b.y, b.score,
+                                     fl | _lib.F_HOST_OUTPUTS), False))
+        t = [torch.from_numpy(np.ascontiguousarray(v)).to(dev) for v in (b.x, b.y, b.score)]
+        t.append(torch.from_numpy(b.box_off.astype(np.int32)).to(dev))
+        t.append(torch.from_numpy(np.ascontiguousarray(b.id_base, dtype=np.int64)).to(dev))
+        dev_in.append(t)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    ctxs = [_lib.Context(0, stream), _lib.Context(0, stream)]
+
+    def submit(c, i):
+        b, t = (b1, b2, b3)[i], dev_in[i]
+        c.submit(b.n_mg, 3, 180, b.box_off, b.id_base, t[0].data_ptr(), t[1].data_ptr(),
+                 t[2].data_ptr(), fl | _lib.F_DEVICE_INPUTS | _lib.F_TIMING,
+                 dev_meta=(t[3].data_ptr(), t[4].data_ptr()))
+
+    order = [0, 1, 2, 0, 2, 1]
+    submit(ctxs[0], order[0])
+    for j, i in enumerate(order):
+        if j + 1 < len(order):
+            submit(ctxs[(j + 1) % 2], order[j + 1])
+        got = snap(ctxs[j % 2].wait(), True)
+        for f in per_mg:
+            np.testing.assert_array_equal(got[f], refs[i][f], err_msg=f"{f} batch {i}")
+        for f, _, _ in per_cl:
+            for a, e in zip(got[f], refs[i][f]):
+                np.testing.assert_array_equal(a.view(np.uint8), e.view(np.uint8), err_msg=f)
+        assert any(n == "k_fused" for n, _ in ctxs[j % 2].kernel_times())
+    for c in ctxs + [ref_ctx]:
+        c.close()
+
+
 def _device_meta_check():
     import torch
     torch.cuda.init()   # torch's HIP runtime first (bench.py order)

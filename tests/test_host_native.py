@@ -27,7 +27,7 @@ def test_abi_exports_match_header():
     so = ctypes.CDLL(_lib.LIB_PATH)
     for name in decl:
         assert hasattr(so, name), name
-    assert _lib.abi_version() == 2
+    assert _lib.abi_version() == 3
 
 
 def _rand_float(rng):

@@ -1,0 +1,24 @@
+#!/usr/bin/env python3
+"""Per-phase marginal PMC counts from a tools/gpu_pmc_ablate.sh log (stopN builds + product).
+
+  python tools/pmc_ablate_delta.py LOG
+"""
+import sys
+
+cur, d = None, {}
+for line in open(sys.argv[1]):
+    if line.startswith("== librepic"):
+        cur = line.split()[1]
+        d[cur] = {}
+    elif cur and "avg=" in line:
+        d[cur][line.split()[0]] = float(line.split("avg=")[1])
+order = sorted(k for k in d if "stop" in k) + ["librepic_gc"]
+keys = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
+        "SQ_LDS_BANK_CONFLICT")
+print(f"{'phase':22s}" + "".join(f"{k[3:]:>16s}" for k in keys) + "   (millions, marginal)")
+prev = {}
+for o in order:
+    v = d[o]
+    print(f"{o:22s}" + "".join(f"{(v[k] - prev.get(k, 0)) / 1e6:16.1f}" for k in keys))
+    prev = v
+print(f"{'total':22s}" + "".join(f"{prev[k] / 1e6:16.1f}" for k in keys))
