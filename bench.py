@@ -266,12 +266,17 @@ def main():
     dbo = torch.from_numpy(batch.box_off.astype(np.int32)).to(dev)
     did = torch.from_numpy(np.ascontiguousarray(batch.id_base, dtype=np.int64)).to(dev)
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    # one explicit stream for every context (torch's default stream handle is 0, with which
+    # each context would create its own stream, and two in-flight steps would run their
+    # kernels concurrently: more throughput, but per-launch kernel times that overlap)
+    tstream = torch.cuda.Stream(dev)
+    stream = tstream.cuda_stream
     ctx = _lib.Context(local, stream)
     flags = _lib.F_DEVICE_INPUTS
-    # pipelined steps (default): two contexts on one stream, rgc_submit / rgc_wait, so the host
-    # side of step i+1 (planning, launch) overlaps the device work of step i; every step still
-    # runs the whole hot path into its own context's outputs and is waited for
+    # pipelined steps (default): two contexts on that one stream, rgc_submit / rgc_wait, so the
+    # host side of step i+1 (planning, launch) overlaps the device work of step i while the
+    # kernels stay serialised; every step runs the whole hot path into its own context's
+    # outputs and is waited for
     pipeline = not (args.host_io or args.no_pipeline)
     ctxs = [ctx, _lib.Context(local, stream)] if pipeline else [ctx]
 

@@ -93,6 +93,8 @@ constexpr int64_t FUSED_MAX_BOXES = 4608;
 // device cursors after the per-micrograph block: [0] clique reservation, [1] edges of finished
 // micrographs, [2] edge-dump reservation (RGC_F_EDGES), [3] spare
 constexpr size_t CUR_BYTES = 32;
+// D_MGOUT / H_MGOUT = per-micrograph SoA block, then two cursor slots of CUR_BYTES: a run
+// uses slot cur_slot and its kernel zeroes the other one for the next run (no memset packet)
 static int lds_blocks(int bytes) { return (bytes + LDS_BLOCK - 1) / LDS_BLOCK; }
 
 // One fused launch configuration: micrographs of <= nmax boxes, forward-edge capacity ecap,
@@ -191,7 +193,12 @@ struct rgc_ctx {
   int64_t cap_cliques = 0;   // capacity of the per-clique output arrays
   int64_t cap_edges = 0;     // RGC_F_EDGES: capacity of the edge dump
   int64_t n_edge_dump = 0;   // RGC_F_EDGES: edges of the last run (host copies in H_EU..)
-  void* cursor_zeroed = nullptr;
+  int cur_slot = 0;          // device cursor slot of the next run (the other one is zeroed)
+  void* slots_at = nullptr;  // D_MGOUT address whose cursor slots are known to be zeroed
+  size_t slots_off = 0;      // ... at this offset
+  int pend_slot = 0;         // cursor slot of the submitted run
+  hipStream_t copy_stream = nullptr;   // rgc_submit: stats copy off the launch stream
+  hipEvent_t ev_k = nullptr;           // rgc_submit: after the fused launch
   hipEvent_t ev_tail = nullptr;    // timing: recorded after each fused pass's stats copy   // fused cursor already cleared on the stream for next run
   std::vector<uint64_t> stamps;   // diagnostic build only
   // rgc_submit / rgc_wait: one run in flight per context
@@ -270,6 +277,34 @@ static int ensure_edges(rgc_ctx* c, int64_t need, int64_t keep) {
   TRY(ensure_dev(c, D_EU, need * 4, keep * 4));
   TRY(ensure_dev(c, D_EV, need * 4, keep * 4));
   TRY(ensure_dev(c, D_EJIOUT, need * 8, keep * 8));
+  return 0;
+}
+
+// Cursor pointers of a fused run (see DCUR_BYTES) and the per-micrograph stats, which the
+// kernel writes straight into host-mapped pinned memory: no copy or memset packet per run.
+struct FusedIo {
+  unsigned long long *cur, *clear;
+  const unsigned long long* h_cur;   // host copy of cur (after the stats copy)
+  int slot;
+  MgOut o;
+};
+static int fused_io(rgc_ctx* c, int n_mg, size_t cur_off, FusedIo* io) {
+  TRY(ensure_host(c, H_MGOUT, cur_off + 2 * CUR_BYTES));
+  TRY(ensure_dev(c, D_MGOUT, cur_off + 2 * CUR_BYTES));
+  char* d = D<char>(c, D_MGOUT);
+  if (c->slots_at != d || c->slots_off != cur_off) {   // new buffer or layout: zero both slots
+    HIPCHK(hipMemsetAsync(d + cur_off, 0, 2 * CUR_BYTES, c->stream));
+    c->slots_at = d;
+    c->slots_off = cur_off;
+    c->cur_slot = 0;
+  }
+  const int sl = c->cur_slot;
+  io->slot = sl;
+  io->cur = reinterpret_cast<unsigned long long*>(d + cur_off + sl * CUR_BYTES);
+  io->clear = reinterpret_cast<unsigned long long*>(d + cur_off + (1 - sl) * CUR_BYTES);
+  io->h_cur = reinterpret_cast<const unsigned long long*>(H<char>(c, H_MGOUT) + cur_off +
+                                                           sl * CUR_BYTES);
+  io->o = mgout_bind(d, n_mg);
   return 0;
 }
 
@@ -540,10 +575,8 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   // the fused kernels' reservation cursor (16 B) sits right after the per-micrograph block,
   // so one copy returns both
   const size_t cur_off = (mgout_bytes(n_mg) + 15) & ~(size_t)15;
-  TRY(ensure_host(c, H_MGOUT, cur_off + CUR_BYTES));
-  TRY(ensure_dev(c, D_MGOUT, cur_off + CUR_BYTES));
+  TRY(ensure_host(c, H_MGOUT, cur_off + 2 * CUR_BYTES));
   const MgOut ho = mgout_bind(H<void>(c, H_MGOUT), n_mg);
-  const MgOut dout = mgout_bind(D<void>(c, D_MGOUT), n_mg);
   std::memset(out, 0, sizeof(*out));
   out->status = ho.status;
   out->cc_max = ho.cc_max;
@@ -577,10 +610,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   if (dev_meta && (!in->dev_box_off || !in->dev_id_base))
     return fail("RGC_F_DEVICE_META needs dev_box_off and dev_id_base");
   TRY(ensure_dev(c, D_MGLIST, 3 * (size_t)n_mg * 4 + 4));
-  unsigned long long* d_cur = reinterpret_cast<unsigned long long*>(
-      static_cast<char*>(D<void>(c, D_MGOUT)) + cur_off);
-  const unsigned long long* h_cur = reinterpret_cast<const unsigned long long*>(
-      static_cast<const char*>(H<void>(c, H_MGOUT)) + cur_off);
+  const unsigned long long* h_cur = nullptr;   // host copy of the fused run's cursor slot
   const int32_t* d_bo = in->dev_box_off;
   const int64_t* d_id = in->dev_id_base;
   if (!dev_meta) {
@@ -654,17 +684,19 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
     for (int attempt = 0; attempt < 2; ++attempt) {
       TRY(ensure_outputs(c, c->cap_cliques, 0, k, want_members, multi != 0));
       if (want_edges) TRY(ensure_edges(c, c->cap_edges, 0));
-      // the previous run cleared the cursor after its last read (off this run's critical
-      // path); otherwise (first run, moved buffer, regrow attempt) clear it here
-      if (attempt > 0 || c->cursor_zeroed != d_cur)
-        HIPCHK(hipMemsetAsync(d_cur, 0, CUR_BYTES, s));
-      c->cursor_zeroed = nullptr;
+      // this run's cursor slot was zeroed by the previous run's kernel (or at allocation);
+      // a regrow attempt re-zeroes it
+      FusedIo io;
+      TRY(fused_io(c, n_mg, cur_off, &io));
+      if (attempt > 0) HIPCHK(hipMemsetAsync(io.cur, 0, CUR_BYTES, s));
+      h_cur = io.h_cur;
       FusedArgs A;
       A.k = k; A.flags = get_cc | (multi << 1) | (want_members ? 32 : 0);
       A.B = B; A.two_b2 = two_b2;
       A.box_off = d_bo; A.id_base = d_id;
-      A.x = x; A.y = y; A.score = sc; A.o = dout;
-      A.cursor = d_cur; A.cap = c->cap_cliques;
+      A.x = x; A.y = y; A.score = sc; A.o = io.o;
+      A.cursor = io.cur; A.cap = c->cap_cliques;
+      A.cursor_clear = io.clear;
       A.rows = D<int32_t>(c, D_ROWS); A.w = D<float>(c, D_W); A.conf = D<float>(c, D_CONF);
       A.consensus = D<int32_t>(c, D_CONS);
       A.members = want_members ? D<int32_t>(c, D_MEMBERS) : nullptr;
@@ -737,7 +769,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
                         (le > 0 ? hipGetErrorString((hipError_t)le) : "unsupported k"));
         }
         TRY(mark(c, "d2h_stats"));
-        HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOUT), D<void>(c, D_MGOUT), cur_off + CUR_BYTES,
+        HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOUT), D<void>(c, D_MGOUT), cur_off + 2 * CUR_BYTES,
                               hipMemcpyDeviceToHost, s));
         if (c->timing) {
           if (!c->ev_tail) HIPCHK(hipEventCreate(&c->ev_tail));
@@ -762,6 +794,8 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
         for (int32_t m : left) todo.push_back(m);
       }
       fused_total = (int64_t)h_cur[0];
+      // this attempt's launches zeroed the other cursor slot: the next run (or regrow) uses it
+      c->cur_slot = 1 - c->cur_slot;
 #ifdef RGC_STAMPS
       const size_t n0w = all0 ? (size_t)n_mg : todo0.size();   // pass 0's workgroups
       c->stamps.resize(n0w * 16);
@@ -917,11 +951,6 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
     TRY(mark(c, "end"));
     HIPCHK(hipStreamSynchronize(s));
   }
-  if (fused_ran) {
-    // clear the cursor for the next run now, while the host is busy elsewhere
-    HIPCHK(hipMemsetAsync(d_cur, 0, CUR_BYTES, s));
-    c->cursor_zeroed = d_cur;
-  }
 
 
   if (c->timing) {
@@ -968,14 +997,10 @@ static int submit_fast(rgc_ctx* c, const rgc_batch_in* in) {
   c->n_ev = 0;
   c->n_edge_dump = 0;
   const size_t cur_off = (mgout_bytes(n_mg) + 15) & ~(size_t)15;
-  TRY(ensure_host(c, H_MGOUT, cur_off + CUR_BYTES));
-  TRY(ensure_dev(c, D_MGOUT, cur_off + CUR_BYTES));
   if (c->cap_cliques < 4096) c->cap_cliques = std::max<int64_t>(4096, N);
   TRY(ensure_outputs(c, c->cap_cliques, 0, k, want_members, multi));
-  unsigned long long* d_cur = reinterpret_cast<unsigned long long*>(
-      static_cast<char*>(D<void>(c, D_MGOUT)) + cur_off);
-  if (c->cursor_zeroed != d_cur) HIPCHK(hipMemsetAsync(d_cur, 0, CUR_BYTES, s));
-  c->cursor_zeroed = nullptr;
+  FusedIo io;
+  TRY(fused_io(c, n_mg, cur_off, &io));
   FusedArgs A;
   A.k = k;
   A.flags = ((flags & RGC_F_GET_CC) ? 1 : 0) | (multi ? 2 : 0) | (want_members ? 32 : 0);
@@ -983,8 +1008,9 @@ static int submit_fast(rgc_ctx* c, const rgc_batch_in* in) {
   A.two_b2 = (double)(2 * in->box_size * in->box_size);
   A.box_off = in->dev_box_off; A.id_base = in->dev_id_base;
   A.x = in->x; A.y = in->y; A.score = in->score;
-  A.o = mgout_bind(D<void>(c, D_MGOUT), n_mg);
-  A.cursor = d_cur; A.cap = c->cap_cliques;
+  A.o = io.o;
+  A.cursor = io.cur; A.cap = c->cap_cliques;
+  A.cursor_clear = io.clear;
   A.rows = D<int32_t>(c, D_ROWS); A.w = D<float>(c, D_W); A.conf = D<float>(c, D_CONF);
   A.consensus = D<int32_t>(c, D_CONS);
   A.members = want_members ? D<int32_t>(c, D_MEMBERS) : nullptr;
@@ -999,15 +1025,22 @@ static int submit_fast(rgc_ctx* c, const rgc_batch_in* in) {
   const int le = launch_fused(s, n_mg, pl.lds, A, false, pl.nt);
   if (le != 0) return fail("fused kernel launch failed (submit): " +
                            std::string(le > 0 ? hipGetErrorString((hipError_t)le) : "unsupported k"));
-  TRY(mark(c, "d2h_stats"));
-  HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOUT), D<void>(c, D_MGOUT), cur_off + CUR_BYTES,
-                        hipMemcpyDeviceToHost, s));
-  if (!c->ev_sub) HIPCHK(hipEventCreateWithFlags(&c->ev_sub, hipEventDisableTiming));
+  c->pend_slot = io.slot;
+  c->cur_slot = 1 - c->cur_slot;   // the launch zeroes the other slot: the next run's
   if (c->timing) {
     if (!c->ev_tail) HIPCHK(hipEventCreate(&c->ev_tail));
     HIPCHK(hipEventRecord(c->ev_tail, s));
   }
-  HIPCHK(hipEventRecord(c->ev_sub, s));
+  // the stats copy runs on the context's copy stream, so the next launch on the main stream
+  // does not wait for it (the next run on THIS context is submitted after rgc_wait)
+  if (!c->copy_stream) HIPCHK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+  if (!c->ev_k) HIPCHK(hipEventCreateWithFlags(&c->ev_k, hipEventDisableTiming));
+  if (!c->ev_sub) HIPCHK(hipEventCreateWithFlags(&c->ev_sub, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(c->ev_k, s));
+  HIPCHK(hipStreamWaitEvent(c->copy_stream, c->ev_k, 0));
+  HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOUT), D<void>(c, D_MGOUT), cur_off + 2 * CUR_BYTES,
+                        hipMemcpyDeviceToHost, c->copy_stream));
+  HIPCHK(hipEventRecord(c->ev_sub, c->copy_stream));
   HIPCHK(hipGetLastError());
   return 1;
 }
@@ -1021,9 +1054,7 @@ static int wait_fast(rgc_ctx* c, rgc_batch_out* out) {
   const size_t cur_off = (mgout_bytes(n_mg) + 15) & ~(size_t)15;
   const MgOut ho = mgout_bind(H<void>(c, H_MGOUT), n_mg);
   const unsigned long long* h_cur = reinterpret_cast<const unsigned long long*>(
-      static_cast<const char*>(H<void>(c, H_MGOUT)) + cur_off);
-  unsigned long long* d_cur = reinterpret_cast<unsigned long long*>(
-      static_cast<char*>(D<void>(c, D_MGOUT)) + cur_off);
+      H<char>(c, H_MGOUT) + cur_off + c->pend_slot * CUR_BYTES);
   bool again = (int64_t)h_cur[0] > c->cap_cliques;
   for (int m = 0; m < n_mg && !again; ++m) again = ho.status[m] >= RGC_ST_DEFER;
   if (again) return 0;
@@ -1047,8 +1078,6 @@ static int wait_fast(rgc_ctx* c, rgc_batch_out* out) {
   out->consensus = D<int32_t>(c, D_CONS);
   out->members = want_members ? D<int32_t>(c, D_MEMBERS) : nullptr;
   out->order = multi ? D<uint8_t>(c, D_ORDER) : nullptr;
-  HIPCHK(hipMemsetAsync(d_cur, 0, CUR_BYTES, c->stream));   // for the next run
-  c->cursor_zeroed = d_cur;
   if (c->timing) {
     c->times.clear();
     c->time_names.clear();
@@ -1103,6 +1132,11 @@ void rgc_ctx_destroy(rgc_ctx* c) {
   for (auto e : c->events) (void)hipEventDestroy(e);
   if (c->ev_tail) (void)hipEventDestroy(c->ev_tail);
   if (c->ev_sub) (void)hipEventDestroy(c->ev_sub);
+  if (c->ev_k) (void)hipEventDestroy(c->ev_k);
+  if (c->copy_stream) {
+    (void)hipStreamSynchronize(c->copy_stream);
+    (void)hipStreamDestroy(c->copy_stream);
+  }
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }

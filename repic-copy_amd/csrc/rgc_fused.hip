@@ -912,6 +912,7 @@ void k_fused(FusedArgs A) {
   S.cbuf = reinterpret_cast<uint16_t*>(smem + L.off_cbuf);
   const int tid = threadIdx.x;
   const int m = A.mg_list ? A.mg_list[blockIdx.x] : (int)blockIdx.x;
+  if (blockIdx.x == 0 && tid < 4 && A.cursor_clear) A.cursor_clear[tid] = 0;   // next run's
 #ifdef RGC_STAMPS
   // diagnostic build only: per-phase s_memtime stamps of thread 0 (never in the product .so)
 #define STAMP(i)                                                                            \

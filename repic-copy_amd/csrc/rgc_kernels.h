@@ -75,6 +75,9 @@ struct FusedArgs {
   const double* score;
   MgOut o;                      // per-micrograph outputs (device)
   unsigned long long* cursor;   // [0] clique-range reservation, [1] edges of finished mgs
+  // cursors of the context's other run slot: zeroed by block 0 for the next run (no memset
+  // packet between runs)
+  unsigned long long* cursor_clear;
   int64_t cap;                  // clique capacity of the output arrays
   int32_t* rows;
   float* w;
