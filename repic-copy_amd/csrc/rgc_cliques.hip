@@ -268,14 +268,7 @@ __global__ __launch_bounds__(WG) void k5_epilogue(CliqueArgs A) {
       s[i] = A.score[mem[i]];
       r[i] = A.vrow[mem[i]];
     }
-#pragma unroll
-    for (int i = 0; i < K; ++i)
-#pragma unroll
-      for (int q = 0; q < K - 1 - i; ++q) {
-        const int a = r[q], b = r[q + 1];
-        r[q] = min(a, b);
-        r[q + 1] = max(a, b);
-      }
+    cmpnet_apply<K, false>(r);   // ascending rows
 #pragma unroll
     for (int i = 0; i < K; ++i) A.rows[j * K + i] = r[i];
     conf32 = (float)median_n<K>(s);   // conf = f32(median score)
@@ -329,7 +322,7 @@ __global__ __launch_bounds__(WG) void k5_epilogue(CliqueArgs A) {
     bool nan = false;
 #pragma unroll
     for (int t = 0; t < NE; ++t) nan |= isnan(I[t]);
-    sort_n<NE>(I);
+    mid_n<NE>(I);
     const double a = I[NE / 2 - 1], b = I[NE / 2];
     med = nan ? NAN : ((a / (two_b2 - a)) + (b / (two_b2 - b))) / 2.0;
   }

@@ -224,35 +224,87 @@ __device__ __forceinline__ bool is_edge(double xa, double ya, double xb, double 
   return *ji > 0.3;
 }
 
-// numpy median (numpy/lib/_function_base_impl.py _median): middle value, or the mean of the
-// two middle values ((a + b) / 2) for even n; NaN if any value is NaN.  Sorting network on a
-// register array (fully unrolled: no scratch).
-template <int N>
-__host__ __device__ __forceinline__ void sort_n(double (&v)[N]) {
-#pragma unroll
-  for (int i = 0; i < N; ++i)
-#pragma unroll
-    for (int j = 0; j < N - 1 - i; ++j) {
-      const double a = v[j], b = v[j + 1];
-      v[j] = fmin(a, b);
-      v[j + 1] = fmax(a, b);
+// Compare-exchange networks on register arrays (fully unrolled: no scratch).  Batcher's
+// odd-even merge sort on the next power of two, comparators that touch the padding (+inf
+// slots above N, never moved) dropped; WANT_MID keeps only the comparators the middle
+// element(s) depend on (backward liveness from outputs N/2, and N/2 - 1 for even N).  Any
+// sorting network yields the same sorted values, so medians are the bubble network's: for
+// k = 8 the 28 pair overlaps take 126 compare-exchanges instead of 378.
+struct CmpNet {
+  int n;
+  unsigned char a[256], b[256];
+};
+template <int N, bool WANT_MID>
+constexpr CmpNet make_cmpnet() {
+  CmpNet all{}, net{};
+  int P = 1;
+  while (P < N) P <<= 1;
+  for (int p = 1; p < P; p += p)
+    for (int k = p; k > 0; k /= 2)
+      for (int j = k % p; j + k < P; j += 2 * k)
+        for (int i = 0; i < k; ++i)
+          if (i + j + k < N && (i + j) / (2 * p) == (i + j + k) / (2 * p)) {
+            all.a[all.n] = (unsigned char)(i + j);
+            all.b[all.n] = (unsigned char)(i + j + k);
+            ++all.n;
+          }
+  bool need[64] = {};
+  for (int i = 0; i < N; ++i) need[i] = !WANT_MID || i == N / 2 || (N % 2 == 0 && i == N / 2 - 1);
+  bool keep[256] = {};
+  for (int c = all.n - 1; c >= 0; --c)
+    if (need[all.a[c]] || need[all.b[c]]) {
+      keep[c] = true;
+      need[all.a[c]] = need[all.b[c]] = true;
     }
+  for (int c = 0; c < all.n; ++c)
+    if (keep[c]) {
+      net.a[net.n] = all.a[c];
+      net.b[net.n] = all.b[c];
+      ++net.n;
+    }
+  return net;
+}
+template <int N, bool WANT_MID>
+struct CmpNetOf {
+  static constexpr CmpNet net = make_cmpnet<N, WANT_MID>();
+};
+// v_min_f64 / v_max_f64 (a total order with -0 < +0 on NaN-free values) and integer min/max
+__host__ __device__ __forceinline__ double cmp_lo(double x, double y) { return fmin(x, y); }
+__host__ __device__ __forceinline__ double cmp_hi(double x, double y) { return fmax(x, y); }
+__host__ __device__ __forceinline__ int cmp_lo(int x, int y) { return x < y ? x : y; }
+__host__ __device__ __forceinline__ int cmp_hi(int x, int y) { return x < y ? y : x; }
+template <int N, bool WANT_MID, typename T>
+__host__ __device__ __forceinline__ void cmpnet_apply(T (&v)[N]) {
+  constexpr int n = CmpNetOf<N, WANT_MID>::net.n;
+#pragma unroll
+  for (int c = 0; c < n; ++c) {
+    const int a = CmpNetOf<N, WANT_MID>::net.a[c], b = CmpNetOf<N, WANT_MID>::net.b[c];
+    const T x = v[a], y = v[b];
+    v[a] = cmp_lo(x, y);
+    v[b] = cmp_hi(x, y);
+  }
 }
 
+// full ascending sort (values only: NaN-free inputs)
+template <int N>
+__host__ __device__ __forceinline__ void sort_n(double (&v)[N]) {
+  cmpnet_apply<N, false>(v);
+}
+// v[N / 2] (and v[N / 2 - 1] for even N) hold the sorted middle values afterwards
+template <int N>
+__host__ __device__ __forceinline__ void mid_n(double (&v)[N]) {
+  cmpnet_apply<N, true>(v);
+}
+
+// numpy median (numpy/lib/_function_base_impl.py _median): middle value, or the mean of the
+// two middle values ((a + b) / 2) for even n; NaN if any value is NaN.
 template <int N>
 __host__ __device__ __forceinline__ double median_n(double (&v)[N]) {
   bool nan = false;
 #pragma unroll
   for (int i = 0; i < N; ++i) nan |= isnan(v[i]);
   if (nan) return NAN;
-#pragma unroll
-  for (int i = 0; i < N; ++i)
-#pragma unroll
-    for (int j = 0; j < N - 1 - i; ++j) {
-      const double a = v[j], b = v[j + 1];
-      v[j] = fmin(a, b);
-      v[j + 1] = fmax(a, b);
-    }
+  mid_n<N>(v);
   if (N & 1) return v[N / 2];
   return (v[N / 2 - 1] + v[N / 2]) / 2.0;
 }

@@ -328,14 +328,7 @@ __device__ __forceinline__ bool fused_epilogue_main(const FCtx<K>& c, int64_t j,
 #pragma unroll
       for (int i = 0; i < K; ++i) s[i] = c.score[c.b0 + li[i]];
     }
-#pragma unroll
-    for (int i = 0; i < K; ++i)
-#pragma unroll
-      for (int q = 0; q < K - 1 - i; ++q) {
-        const int a = r[q], b = r[q + 1];
-        r[q] = min(a, b);
-        r[q + 1] = max(a, b);
-      }
+    cmpnet_apply<K, false>(r);   // ascending rows
 #pragma unroll
     for (int i = 0; i < K; ++i) c.rows[j * K + i] = r[i];
     {
@@ -360,7 +353,7 @@ __device__ __forceinline__ bool fused_epilogue_main(const FCtx<K>& c, int64_t j,
       bool nan = false;
 #pragma unroll
       for (int t = 0; t < NE; ++t) nan |= isnan(Is[t]);
-      sort_n<NE>(Is);
+      mid_n<NE>(Is);
       const double a = Is[NE / 2 - 1], b = Is[NE / 2];
       med = nan ? NAN : ((a / (c.two_b2 - a)) + (b / (c.two_b2 - b))) / 2.0;
     }
