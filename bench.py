@@ -29,7 +29,7 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
-DEFAULT_MG = {"C2": 10000, "C3": 1000, "C4": 12500, "C5": 64}
+DEFAULT_MG = {"C2": 10000, "C3": 4000, "C4": 12500, "C5": 64}
 
 
 def fused_compulsory_bytes(N, C, k, V, n_mg):
