@@ -271,6 +271,8 @@ struct CmpNetOf {
 // v_min_f64 / v_max_f64 (a total order with -0 < +0 on NaN-free values) and integer min/max
 __host__ __device__ __forceinline__ double cmp_lo(double x, double y) { return fmin(x, y); }
 __host__ __device__ __forceinline__ double cmp_hi(double x, double y) { return fmax(x, y); }
+__host__ __device__ __forceinline__ float cmp_lo(float x, float y) { return fminf(x, y); }
+__host__ __device__ __forceinline__ float cmp_hi(float x, float y) { return fmaxf(x, y); }
 __host__ __device__ __forceinline__ int cmp_lo(int x, int y) { return x < y ? x : y; }
 __host__ __device__ __forceinline__ int cmp_hi(int x, int y) { return x < y ? y : x; }
 template <int N, bool WANT_MID, typename T>
@@ -291,8 +293,8 @@ __host__ __device__ __forceinline__ void sort_n(double (&v)[N]) {
   cmpnet_apply<N, false>(v);
 }
 // v[N / 2] (and v[N / 2 - 1] for even N) hold the sorted middle values afterwards
-template <int N>
-__host__ __device__ __forceinline__ void mid_n(double (&v)[N]) {
+template <int N, typename T>
+__host__ __device__ __forceinline__ void mid_n(T (&v)[N]) {
   cmpnet_apply<N, true>(v);
 }
 

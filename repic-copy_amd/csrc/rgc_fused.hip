@@ -22,6 +22,8 @@
 //   P6 clique DFS fill + epilogue + COO rows                 (:169-202)
 #pragma clang fp contract(off)
 
+#include <type_traits>
+
 #include "rgc_device.h"
 #include "rgc_kernels.h"
 
@@ -142,6 +144,7 @@ struct FCtx {
   int m, b0, n;
   int64_t idb;       // global id of local box 0
   bool set_order;    // networkx iterates set(sorted(clique)) (2k < |G|)
+  bool intp;         // integer coordinates (P2) and B <= 2896: exact f32 overlaps in P6
   int64_t out;       // next clique index within the micrograph (fill)
   int64_t c0, c1;    // clique chunk being buffered in cbuf (fill)
   int64_t count;
@@ -304,20 +307,32 @@ __device__ __forceinline__ uint64_t ins_key(const FCtx<K>& c, int u) {
 // returns true when the consensus needs the node-iteration order (a degree tie, or
 // --multi_out), which fused_epilogue_order computes in a second, rarely-taken pass (its
 // 64-bit hashing stays out of this pass's register budget).
-template <int K, bool W>
+// INTP (integer coordinates below 2^23, B <= 2896, f32 layout): every overlap B - |dx| and
+// product is an integer below 2^24, exact in f32, so the overlaps, their median network and the
+// f32 degree JIs (2 B^2 - I exact too) run on floats; the median overlaps are converted back
+// to f64 exactly for the reference's divisions.  Same results, half the registers.
+template <int K, bool W, bool INTP = false>
 __device__ __forceinline__ bool fused_epilogue_main(const FCtx<K>& c, int64_t j,
                                                     const int (&mem)[K]) {
   constexpr int NE = K * (K - 1) / 2;
-  double I[NE];   // overlaps of the member pairs (a < b) in reference op order
+  using OT = typename std::conditional<INTP, float, double>::type;
+  OT I[NE];       // overlaps of the member pairs (a < b) in reference op order
   int li[K];      // local (file-order) indices: id order
   {
-    double s[K], xs[K], ys[K];
+    double s[K];
+    OT xs[K], ys[K];
     int r[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-      const double2 xy = ld_xy<W>(c.S, mem[i]);
-      xs[i] = xy.x;
-      ys[i] = xy.y;
+      if constexpr (INTP) {
+        const float2 xy = reinterpret_cast<const float2*>(c.S.sxy)[mem[i]];
+        xs[i] = xy.x;
+        ys[i] = xy.y;
+      } else {
+        const double2 xy = ld_xy<W>(c.S, mem[i]);
+        xs[i] = xy.x;
+        ys[i] = xy.y;
+      }
       li[i] = c.S.citems[mem[i]];
       r[i] = c.S.vrank[mem[i]];
     }
@@ -336,17 +351,33 @@ __device__ __forceinline__ bool fused_epilogue_main(const FCtx<K>& c, int64_t j,
 #pragma unroll
       for (int a = 0; a < K; ++a)
 #pragma unroll
-        for (int b = a + 1; b < K; ++b) I[t++] = overlap(xs[a], ys[a], xs[b], ys[b], c.B);
+        for (int b = a + 1; b < K; ++b) {
+          if constexpr (INTP) {
+            const float Bf = (float)c.B;
+            I[t++] = fmaxf(Bf - fabsf(xs[a] - xs[b]), 0.0f) * fmaxf(Bf - fabsf(ys[a] - ys[b]), 0.0f);
+          } else {
+            I[t++] = overlap(xs[a], ys[a], xs[b], ys[b], c.B);
+          }
+        }
     }
     // conf = f32(median score); w = f32(f64(conf) * median JI) where median JI = JI of the
     // median overlap (JI = I / (2 B^2 - I) is non-decreasing in I, so sorting by I sorts the
     // JIs): one or two reference divisions instead of one per pair
     const double cf = median_n<K>(s);
-    double Is[NE];
+    OT Is[NE];
 #pragma unroll
     for (int t = 0; t < NE; ++t) Is[t] = I[t];
     double med;
-    if (NE & 1) {
+    if constexpr (INTP) {   // finite integers: no NaN
+      mid_n<NE>(Is);
+      if (NE & 1) {
+        med = (double)Is[NE / 2];
+        med = med / (c.two_b2 - med);
+      } else {
+        const double a = (double)Is[NE / 2 - 1], b = (double)Is[NE / 2];
+        med = ((a / (c.two_b2 - a)) + (b / (c.two_b2 - b))) / 2.0;
+      }
+    } else if (NE & 1) {
       med = median_n<NE>(Is);   // sorted copy's middle element
       med = med / (c.two_b2 - med);
     } else {
@@ -378,7 +409,9 @@ __device__ __forceinline__ bool fused_epilogue_main(const FCtx<K>& c, int64_t j,
     for (int a = 0; a < K; ++a)
 #pragma unroll
       for (int b = a + 1; b < K; ++b) {
-        const float jf = (float)I[t] * __builtin_amdgcn_rcpf((float)(c.two_b2 - I[t]));
+        float jf;
+        if constexpr (INTP) jf = I[t] * __builtin_amdgcn_rcpf((float)c.two_b2 - I[t]);
+        else jf = (float)I[t] * __builtin_amdgcn_rcpf((float)(c.two_b2 - I[t]));
         deg[a] += jf;
         deg[b] += jf;
         ++t;
@@ -1442,6 +1475,7 @@ void k_fused(FusedArgs A) {
     // the DFS per chunk of <= cq_cap cliques.
     // scores of the clique vertices into LDS by row rank when they fit in parent..scell
     c.S.vstaged = 8 * H.V <= L.off_citems - L.off_parent;
+    c.intp = intp && A.B <= 2896.0;
     if (c.S.vstaged) {
       for (int t = tid; t < n; t += FWG)
         if (S.flags[t] == 3) c.S.vscore[S.vrank[t]] = c.score[b0 + S.citems[t]];
@@ -1505,7 +1539,10 @@ void k_fused(FusedArgs A) {
       for (int sl = tid; sl < c1 - c0; sl += FWG) {
         int mem[K];
         clique_members(sl, mem);
-        if (fused_epilogue_main<K, W>(c, obase + (c0 + sl), mem)) {
+        bool order;
+        if (!W && c.intp) order = fused_epilogue_main<K, W, true>(c, obase + (c0 + sl), mem);
+        else order = fused_epilogue_main<K, W, false>(c, obase + (c0 + sl), mem);
+        if (order) {
           c.cq_ord[sl] |= 0x8000;
           any = true;
         }
