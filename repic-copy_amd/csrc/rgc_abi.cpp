@@ -59,7 +59,7 @@ enum DevBufId {
   D_BOXOFF, D_CELLOFF, D_P0OFF, D_IDBASE, D_GRID, D_CELLSTART, D_SX, D_SY, D_SBOX, D_SPICK, D_SMG, D_BMG,
   D_BPICK, D_FWDCNT, D_FWDOFF, D_TILES, D_TOTAL, D_EDST, D_EJI, D_PARENT, D_HASEDGE, D_CSIZE,
   D_STAT, D_INSKEY, D_COMPMIN, D_CCOUNT, D_COFF, D_INCL, D_VLIST, D_VSORT, D_VROW, D_BOFF, D_RLO, D_ADJG, D_RBOUND, D_RFLAG, D_DFSMG, D_ROOTBOX, D_EXLIST,
-  D_LCNT, D_LOFF, D_LROOT0, D_LROOT1, D_LM0, D_LM1, D_LP0, D_LP1,
+  D_LCNT, D_LOFF, D_LROOT0, D_LROOT1, D_LM0, D_LM1, D_LP0, D_LP1, D_PK,
   // RGC_F_EDGES test hook
   D_EU, D_EV, D_EJIOUT,
   // score_detections raster
@@ -449,6 +449,7 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   A.parent = D<int32_t>(c, D_PARENT); A.st = D<MgStat>(c, D_STAT);
   A.ins_key = D<unsigned long long>(c, D_INSKEY); A.clique_off = D<int64_t>(c, D_COFF);
   A.vrow = D<int32_t>(c, D_VROW);
+  A.pk = nullptr;
   A.ccount = D<int32_t>(c, D_CCOUNT); A.in_clique = D<uint8_t>(c, D_INCL);
   A.adjg = D<uint64_t>(c, D_ADJG); A.rbound = D<uint64_t>(c, D_RBOUND);
   A.rflag = D<uint8_t>(c, D_RFLAG); A.dfs_mg = D<uint8_t>(c, D_DFSMG); A.dfs_base = 0;
@@ -530,6 +531,10 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   A.exlist = D<int64_t>(c, D_EXLIST);
   A.excount = reinterpret_cast<unsigned long long*>(d_tot + 3);   // rank scan total is dead
   HIPCHK(hipMemsetAsync(A.excount, 0, 8, s));
+  TRY(ensure_dev(c, D_PK, (size_t)N * 32));
+  A.pk = D<double>(c, D_PK);
+  TRY(mark(c, "k5_pack"));
+  launch_clique_pack(s, (int)N, A);
   TRY(mark(c, "k5_epilogue"));
   launch_clique_epilogue(s, A);
   TRY(mark(c, "k5_ranges"));

@@ -243,6 +243,85 @@ __global__ __launch_bounds__(WG) void k5_ranges(CliqueArgs A, int64_t C1, int64_
   rhi[m] = b[1];
 }
 
+// Weighted-degree consensus candidate and median JI of one clique from its member coordinates
+// (get_cliques.py:169-190).  T = float only for integer coordinates below 2^23 and B <= 2896:
+// every overlap B - |dx| (and their products, and 2 B^2 - I) is then an exact float.
+template <int K, typename T>
+__device__ __forceinline__ void epi_core(const T (&xs)[K], const T (&ys)[K], T B, double two_b2,
+                                         bool multi, bool* exact, int* arg, double* med) {
+  constexpr int NE = K * (K - 1) / 2;
+  constexpr bool F = sizeof(T) == 4;
+  T I[NE];   // member-pair overlaps (a < b), reference op order
+  {
+    int t = 0;
+#pragma unroll
+    for (int a = 0; a < K; ++a)
+#pragma unroll
+      for (int b = a + 1; b < K; ++b) {
+        if constexpr (F)
+          I[t++] = fmaxf(B - fabsf(xs[a] - xs[b]), 0.0f) * fmaxf(B - fabsf(ys[a] - ys[b]), 0.0f);
+        else
+          I[t++] = overlap(xs[a], ys[a], xs[b], ys[b], B);
+      }
+  }
+  if (!multi) {
+    // weighted degrees from f32 JIs: f32 operands (2^-24 each) and v_rcp_f32 (1 ulp) give
+    // < 4e-7 per JI <= 1, < 5.5e-6 per sum of <= 7 terms with its f32 additions; a maximum
+    // clear by 3e-5 is the reference's, anything closer takes the exact f64 pass (ties)
+    float deg[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) deg[i] = 0.0f;
+    int t = 0;
+#pragma unroll
+    for (int a = 0; a < K; ++a)
+#pragma unroll
+      for (int b = a + 1; b < K; ++b) {
+        float jf;
+        if constexpr (F) jf = I[t] * __builtin_amdgcn_rcpf((float)two_b2 - I[t]);
+        else jf = (float)I[t] * __builtin_amdgcn_rcpf((float)(two_b2 - I[t]));
+        deg[a] += jf;
+        deg[b] += jf;
+        ++t;
+      }
+    float d1 = deg[0], d2 = -INFINITY;
+    int ag = 0;
+#pragma unroll
+    for (int i = 1; i < K; ++i) {
+      const float d = deg[i];
+      d2 = d > d1 ? d1 : fmaxf(d2, d);
+      ag = d > d1 ? i : ag;
+      d1 = fmaxf(d1, d);
+    }
+    *arg = ag;
+    *exact = !(d1 - d2 > 3e-5f);
+  }
+  // median JI = JI of the median overlap (JI is non-decreasing in I and the f64 quotient
+  // keeps that order): one or two reference divisions; I is partially sorted in place
+  bool nan = false;
+  if constexpr (!F) {
+#pragma unroll
+    for (int t = 0; t < NE; ++t) nan |= isnan(I[t]);
+  }
+  mid_n<NE>(I);
+  if (NE & 1) {
+    const double m = (double)I[NE / 2];
+    *med = nan ? NAN : m / (two_b2 - m);
+  } else {
+    const double a = (double)I[NE / 2 - 1], b = (double)I[NE / 2];
+    *med = nan ? NAN : ((a / (two_b2 - a)) + (b / (two_b2 - b))) / 2.0;
+  }
+}
+
+// One 32-byte record per box for the epilogue's member gathers (x, y, score, row rank in the
+// low word of the last slot): two 16-byte loads per member instead of four scattered ones.
+__global__ __launch_bounds__(WG) void k5_pack(int N, CliqueArgs A) {
+  const int i = blockIdx.x * WG + threadIdx.x;
+  if (i >= N) return;
+  double2* o = reinterpret_cast<double2*>(A.pk) + 2 * (int64_t)i;
+  o[0] = make_double2(A.x[i], A.y[i]);
+  o[1] = make_double2(A.score[i], __longlong_as_double((long long)(uint32_t)A.vrow[i]));
+}
+
 // ILP epilogue, one thread per clique (get_cliques.py:164-202): COO rows (vertex ranks by
 // (x, y, id), ascending), conf = f32(median score), w = f32(f64(conf) * median JI), and the
 // consensus box (largest weighted degree, CPython set-order tie-break); --multi_out: the
@@ -263,10 +342,12 @@ __global__ __launch_bounds__(WG) void k5_epilogue(CliqueArgs A) {
     int r[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-      xs[i] = A.x[mem[i]];
-      ys[i] = A.y[mem[i]];
-      s[i] = A.score[mem[i]];
-      r[i] = A.vrow[mem[i]];
+      const double2* pk = reinterpret_cast<const double2*>(A.pk) + 2 * (int64_t)mem[i];
+      const double2 p0 = pk[0], p1 = pk[1];
+      xs[i] = p0.x;
+      ys[i] = p0.y;
+      s[i] = p1.x;
+      r[i] = (int)(uint32_t)__double_as_longlong(p1.y);
     }
     cmpnet_apply<K, false>(r);   // ascending rows
 #pragma unroll
@@ -274,57 +355,24 @@ __global__ __launch_bounds__(WG) void k5_epilogue(CliqueArgs A) {
     conf32 = (float)median_n<K>(s);   // conf = f32(median score)
   }
   const double B = A.B, two_b2 = A.two_b2;
-  double I[NE];   // member-pair overlaps (a < b), reference op order
-  {
-    int t = 0;
-#pragma unroll
-    for (int a = 0; a < K; ++a)
-#pragma unroll
-      for (int b = a + 1; b < K; ++b) I[t++] = overlap(xs[a], ys[a], xs[b], ys[b], B);
-  }
   const bool multi = (A.flags & 2) != 0;
   int arg = 0;
   bool exact = multi;
-  if (!multi) {
-    // weighted degrees from f32 JIs: f32 operands (2^-24 each) and v_rcp_f32 (1 ulp) give
-    // < 4e-7 per JI <= 1, < 5.5e-6 per sum of <= 7 terms with its f32 additions; a maximum
-    // clear by 3e-5 is the reference's, anything closer takes the exact f64 pass (ties)
-    float deg[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i) deg[i] = 0.0f;
-    int t = 0;
-#pragma unroll
-    for (int a = 0; a < K; ++a)
-#pragma unroll
-      for (int b = a + 1; b < K; ++b) {
-        const float jf = (float)I[t] * __builtin_amdgcn_rcpf((float)(two_b2 - I[t]));
-        deg[a] += jf;
-        deg[b] += jf;
-        ++t;
-      }
-    float d1 = deg[0], d2 = -INFINITY;
-#pragma unroll
-    for (int i = 1; i < K; ++i) {
-      const float d = deg[i];
-      d2 = d > d1 ? d1 : fmaxf(d2, d);
-      arg = d > d1 ? i : arg;
-      d1 = fmaxf(d1, d);
-    }
-    exact = !(d1 - d2 > 3e-5f);
-  }
-  // median JI = JI of the median overlap (JI is non-decreasing in I and the f64 quotient
-  // keeps that order): one or two reference divisions; I is sorted in place
   double med;
-  if (NE & 1) {
-    med = median_n<NE>(I);
-    med = med / (two_b2 - med);
-  } else {
-    bool nan = false;
+  // integer coordinates below 2^23 and B <= 2896: overlaps, their median network and the
+  // degree JIs on exact floats (as the fused epilogue's INTP path); otherwise f64
+  bool intok = B >= 1.0 && B <= 2896.0 && B == floor(B);
 #pragma unroll
-    for (int t = 0; t < NE; ++t) nan |= isnan(I[t]);
-    mid_n<NE>(I);
-    const double a = I[NE / 2 - 1], b = I[NE / 2];
-    med = nan ? NAN : ((a / (two_b2 - a)) + (b / (two_b2 - b))) / 2.0;
+  for (int i = 0; i < K; ++i)
+    intok = intok && xs[i] == rint(xs[i]) && ys[i] == rint(ys[i]) && fabs(xs[i]) < 0x1p23 &&
+            fabs(ys[i]) < 0x1p23;
+  if (intok) {
+    float xf[K], yf[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) { xf[i] = (float)xs[i]; yf[i] = (float)ys[i]; }
+    epi_core<K, float>(xf, yf, (float)B, two_b2, multi, &exact, &arg, &med);
+  } else {
+    epi_core<K, double>(xs, ys, B, two_b2, multi, &exact, &arg, &med);
   }
   A.w[j] = (float)((double)conf32 * med);
   A.conf[j] = conf32;
@@ -447,6 +495,10 @@ int launch_clique_epilogue(hipStream_t stream, const CliqueArgs& A) {
     default: return -1;
   }
   return 0;
+}
+
+void launch_clique_pack(hipStream_t stream, int N, const CliqueArgs& A) {
+  if (N > 0) hipLaunchKernelGGL(k5_pack, dim3((N + WG - 1) / WG), dim3(WG), 0, stream, N, A);
 }
 
 void launch_clique_ranges(hipStream_t stream, const CliqueArgs& A, int64_t C1, int64_t* rlo,

@@ -134,6 +134,7 @@ struct CliqueArgs {
   const unsigned long long* ins_key;
   const int64_t* clique_off;
   const int32_t* vrow;
+  double* pk;                // [N][4] epilogue gather record: x, y, score, vrow (k5_pack)
   int32_t* ccount;
   uint8_t* in_clique;
   uint64_t* adjg;            // [E] neighbourhood adjacency row of each root's i-th neighbour
@@ -188,6 +189,7 @@ void launch_clique_setup(hipStream_t stream, int N, const CliqueArgs& A);
 int launch_clique_level(hipStream_t stream, bool first, bool leaf, bool fill, const CliqueArgs& A,
                         const LevelArgs& L);
 int launch_clique_epilogue(hipStream_t stream, const CliqueArgs& A);
+void launch_clique_pack(hipStream_t stream, int N, const CliqueArgs& A);
 void launch_clique_ranges(hipStream_t stream, const CliqueArgs& A, int64_t C1, int64_t* rlo,
                           int64_t* rhi);
 int launch_cliques_dfs(hipStream_t stream, bool fill, int N, const CliqueArgs& A);
