@@ -997,18 +997,22 @@ void k_fused(FusedArgs A) {
     }
     for (int i = tid + RB * FWG; i < n; i += FWG) fn(i, A.x[b0 + i], A.y[b0 + i]);
   };
-  double mnx = INFINITY, mny = INFINITY, mxx = -INFINITY, mxy = -INFINITY;
+  // bounding box on floats for the f32 layout (exact there; a micrograph with inexact
+  // coordinates is deferred to the f64 layout, where it is computed in f64)
+  using BT = typename std::conditional<W, double, float>::type;
+  BT bmnx = INFINITY, bmny = INFINITY, bmxx = -INFINITY, bmxy = -INFINITY;
   bool inexact = false;   // a coordinate not exactly representable as f32 (NaN excepted)
   bool nonint = false;    // a finite box with a coordinate off the integer grid (-2^23, 2^23)
   each_box([&](int, double xv, double yv) {
     if (isfinite(xv) && isfinite(yv)) {
-      mnx = fmin(mnx, xv); mxx = fmax(mxx, xv);
-      mny = fmin(mny, yv); mxy = fmax(mxy, yv);
+      bmnx = fmin(bmnx, (BT)xv); bmxx = fmax(bmxx, (BT)xv);
+      bmny = fmin(bmny, (BT)yv); bmxy = fmax(bmxy, (BT)yv);
       nonint |= xv != rint(xv) || yv != rint(yv) || fabs(xv) >= 0x1p23 || fabs(yv) >= 0x1p23;
     }
     if (!W) inexact |= ((double)(float)xv != xv && xv == xv) || ((double)(float)yv != yv && yv == yv);
   });
-  if (inexact) mnx = -INFINITY;   // (impossible otherwise) carried through the min reduction
+  if (inexact) bmnx = -INFINITY;   // (impossible otherwise) carried through the min reduction
+  double mnx, mny, mxx, mxy;
   // P1's packed bucket counters (the whole cell-start region of the size class), union-find
   // parents, node flags and P2's packed CC-size counters are set up here, so the bounding-box
   // barrier orders them too
@@ -1024,13 +1028,14 @@ void k_fused(FusedArgs A) {
     for (int q = tid; q < (n + 1) / 2; q += FWG) ccsz[q] = 0;
   }
   {
-    double v[4] = {mnx, mny, -mxx, -mxy};
+    BT bv[4] = {bmnx, bmny, -bmxx, -bmxy};
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      v[r] = wave_incl_scan(v[r], [](double a, double b) { return fmin(a, b); });
+      bv[r] = wave_incl_scan(bv[r], [](BT a, BT b) { return fmin(a, b); });
     if ((tid & 63) == 63)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) H.red4[r][tid >> 6] = v[r];
+      for (int r = 0; r < 4; ++r) H.red4[r][tid >> 6] = (double)bv[r];
+    double v[4];
     const bool wn = __any(nonint);
     if ((tid & 63) == 0) H.nonint[tid >> 6] = wn ? 1 : 0;
     __syncthreads();
@@ -1431,13 +1436,18 @@ void k_fused(FusedArgs A) {
     uint16_t* bcnt = S.parent;
     uint32_t* bw = reinterpret_cast<uint32_t*>(S.parent);
     uint16_t* blist = S.scell;
-    const double minx = H.minx, xbs = H.xbs;
-    auto xbucket = [&](double xv) { return (int)fmin((xv - minx) * xbs, (double)(n - 1)); };
+    // f32 layout: coordinates exact as floats, so bucket and (x, y) comparisons run on floats
+    // (same order); the bucket map only has to be monotone in x and the same in every pass
+    using CT = typename std::conditional<W, double, float>::type;
+    using CT2 = typename std::conditional<W, double2, float2>::type;
+    auto ld = [&](int t) -> CT2 { return reinterpret_cast<const CT2*>(S.sxy)[t]; };
+    const CT minx = (CT)H.minx, xbs = (CT)H.xbs, nlast = (CT)(n - 1);
+    auto xbucket = [&](CT xv) { return (int)fmin((xv - minx) * xbs, nlast); };
     for (int q = tid; q <= (n + 1) / 2; q += FWG) bw[q] = 0;
     __syncthreads();
     for (int t = tid; t < n; t += FWG) {
       if (S.flags[t] != 3) continue;
-      const int q = xbucket(ld_xy<W>(S, t).x);
+      const int q = xbucket(ld(t).x);
       const int sh = 16 * (q & 1);
       S.vrank[t] = (uint16_t)((atomicAdd(&bw[q >> 1], 1u << sh) >> sh) & 0xFFFFu);
     }
@@ -1446,19 +1456,19 @@ void k_fused(FusedArgs A) {
     if (tid == 0) { H.V = (int)V; bcnt[n] = (uint16_t)V; }
     for (int t = tid; t < n; t += FWG) {
       if (S.flags[t] != 3) continue;
-      blist[bcnt[xbucket(ld_xy<W>(S, t).x)] + S.vrank[t]] = (uint16_t)t;
+      blist[bcnt[xbucket(ld(t).x)] + S.vrank[t]] = (uint16_t)t;
     }
     __syncthreads();
     for (int t = tid; t < n; t += FWG) {
       if (S.flags[t] != 3) continue;
       const int vi = S.citems[t];
-      const double2 v = ld_xy<W>(S, t);
+      const CT2 v = ld(t);
       const int b = xbucket(v.x);
       const int lo = bcnt[b], hi = bcnt[b + 1];
       uint32_t rk = lo;
       for (int u = lo; u < hi; ++u) {
         const int tu = blist[u];
-        const double2 w = ld_xy<W>(S, tu);
+        const CT2 w = ld(tu);
         const int ui = S.citems[tu];
         rk += (w.x < v.x) || (w.x == v.x && (w.y < v.y || (w.y == v.y && ui < vi)));
       }
