@@ -546,7 +546,12 @@ template <int K>
 struct BfsOut {
   int64_t C;        // cliques, or -1: a level did not fit (caller falls back to the DFS)
   int lvl[K + 1];   // byte offset in q of each level's entries (2..K)
+  float fit;        // capacity / demand: of the level that overflowed (C = -1, < 1), else the
+                    // smallest over the levels (>= 1)
 };
+__device__ __forceinline__ float bfs_fit(int64_t need, int64_t have) {
+  return need > 0 ? (float)max(have, (int64_t)0) / (float)need : 1.0f;
+}
 
 // REWALK (P6 re-run of a root chunk): the split array and the union-find parents are dead by
 // then, so first segments come from a binary search for the next picker's first position and
@@ -582,7 +587,15 @@ struct BfsLevel {
     int (&lvl)[K + 1] = out.lvl;
     // temps of this level at the top of q
     const int tb = (qbytes - 8 * (int)(nD + 1)) & ~7;
-    if (nD > 65535 || tb < lvl[D] + 4 * (int)nD) { out.C = -1; return out; }
+    {
+      const float f = fminf(bfs_fit(nD, 65535), bfs_fit(12 * nD, qbytes - lvl[D] - 8));
+      out.fit = fminf(out.fit, f);
+      if (nD > 65535 || tb < lvl[D] + 4 * (int)nD) {
+        out.C = -1;
+        out.fit = fminf(f, 0.999f);
+        return out;
+      }
+    }
     uint32_t* MK = reinterpret_cast<uint32_t*>(q + tb);
     uint32_t* CN = MK + nD;
     for (int e = tid; e < nD; e += NT) {
@@ -607,7 +620,15 @@ struct BfsLevel {
     const int64_t nN = block_scan_dpp<NT>(CN, (int)nD, H.red64);
     constexpr bool last = D + 1 == K;
     const int nb = (lvl[D] + 4 * (int)nD + 3) & ~3;   // next level starts here
-    if (nN > 65535 || nN * (last ? 6 : 4) > tb - nb) { out.C = -1; return out; }
+    {
+      const float f = fminf(bfs_fit(nN, 65535), bfs_fit(nN * (last ? 6 : 4), tb - nb));
+      out.fit = fminf(out.fit, f);
+      if (nN > 65535 || nN * (last ? 6 : 4) > tb - nb) {
+        out.C = -1;
+        out.fit = fminf(f, 0.999f);
+        return out;
+      }
+    }
     for (int e = tid; e < nD; e += NT) {
       int mm[K];
       prefix(q, lvl, (uint32_t)e, mm);
@@ -660,6 +681,7 @@ __device__ __forceinline__ BfsOut<K> bfs_cliques(const FShared& S, FusedHdr& H, 
                                                  const int (&pp)[K + 1]) {
   BfsOut<K> out;
   out.C = -1;
+  out.fit = 4.0f;
 #pragma unroll
   for (int d = 0; d <= K; ++d) out.lvl[d] = 0;
   const int nr = r1 - r0;
@@ -680,7 +702,11 @@ __device__ __forceinline__ BfsOut<K> bfs_cliques(const FShared& S, FusedHdr& H, 
   __syncthreads();
   const int64_t n2 = block_scan_dpp<NT>(cnt, nr, H.red64);
   constexpr bool last = K == 2;
-  if (n2 > 65535 || n2 * (last ? 6 : 4) > qbytes) return out;
+  out.fit = fminf(bfs_fit(n2, 65535), bfs_fit(n2 * (last ? 6 : 4), qbytes));
+  if (n2 > 65535 || n2 * (last ? 6 : 4) > qbytes) {
+    out.fit = fminf(out.fit, 0.999f);
+    return out;
+  }
   for (int i = tid; i < nr; i += NT) {
     const int r = r0 + i;
     if (!root_ok(r)) continue;
@@ -1367,8 +1393,10 @@ void k_fused(FusedArgs A) {
       bo = bfs_cliques<K, false, NT>(S, H, q, qbytes, r0, r0 + len, get_cc, (uint32_t)target, tid,
                                  c.pp);
       if (bo.C < 0) {
+        // shrink to the estimated fit of the overflowing level (demand grows about linearly
+        // with the roots), with a small margin; strictly smaller each time
         ok = K >= 4 && len > 1;
-        len = (len + 1) / 2;
+        len = max(1, min(len - 1, (int)((float)len * bo.fit * 0.95f)));
         continue;
       }
       if (nch == maxch) { ok = false; break; }
@@ -1376,7 +1404,8 @@ void k_fused(FusedArgs A) {
       r0 += len;
       ++nch;
       if (tid == 0) { chtab[2 * nch] = (uint32_t)r0; chtab[2 * nch + 1] = (uint32_t)C; }
-      len = 2 * len;
+      // next chunk: as many roots as the tightest level of this one leaves room for
+      len = max(len + 1, (int)((float)len * fminf(bo.fit, 2.0f) * 0.95f));
     }
     if (!ok) { nch = 0; C = 0; bo.C = -1; }
   }
@@ -1408,6 +1437,12 @@ void k_fused(FusedArgs A) {
   }
   c.S.cbuf = S.cbuf;
   STAMP(8);   // cliques
+#ifdef RGC_STAMPS
+  if (tid == 0) {   // diagnostic build: root chunks of the BFS (0 = DFS fallback) and cliques
+    A.stamps[(int64_t)blockIdx.x * 16 + 14] = (unsigned long long)nch;
+    A.stamps[(int64_t)blockIdx.x * 16 + 15] = (unsigned long long)C;
+  }
+#endif
   if (tid == 0) {
     H.C = C;
     if (C == 0) {

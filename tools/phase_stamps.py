@@ -34,7 +34,11 @@ f.restype = C.c_int64
 n = f(ctx._p, None, 0)
 buf = (C.c_uint64 * n)()
 f(ctx._p, buf, n)
-st = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 16).astype(np.int64)[:, :13]
+raw = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 16).astype(np.int64)
+st = raw[:, :13]
+nch, ncl = raw[:, 14], raw[:, 15]
+print(f"BFS root chunks per micrograph: mean {nch.mean():.2f} p50 {np.median(nch):.0f} "
+      f"max {nch.max()} (0 = per-root DFS fallback: {(nch == 0).sum()}); cliques mean {ncl.mean():.0f}")
 names = ["P0 load+bbox", "P1 grid+sort", "P2a count", "P2b fwd scan", "P2c fill",
          "P3a union", "P3b CC stats", "P4a DFS+queue", "P4b scan+reserve", "P5 rank",
          "P6a score staging", "P6b epilogue"]
