@@ -587,14 +587,14 @@ struct BfsLevel {
     int (&lvl)[K + 1] = out.lvl;
     // temps of this level at the top of q
     const int tb = (qbytes - 8 * (int)(nD + 1)) & ~7;
-    {
+    if (K >= 4) {   // (K = 3 runs one attempt: no chunk sizing)
       const float f = fminf(bfs_fit(nD, 65535), bfs_fit(12 * nD, qbytes - lvl[D] - 8));
       out.fit = fminf(out.fit, f);
-      if (nD > 65535 || tb < lvl[D] + 4 * (int)nD) {
-        out.C = -1;
-        out.fit = fminf(f, 0.999f);
-        return out;
-      }
+    }
+    if (nD > 65535 || tb < lvl[D] + 4 * (int)nD) {
+      out.C = -1;
+      out.fit = fminf(out.fit, 0.999f);
+      return out;
     }
     uint32_t* MK = reinterpret_cast<uint32_t*>(q + tb);
     uint32_t* CN = MK + nD;
@@ -620,14 +620,14 @@ struct BfsLevel {
     const int64_t nN = block_scan_dpp<NT>(CN, (int)nD, H.red64);
     constexpr bool last = D + 1 == K;
     const int nb = (lvl[D] + 4 * (int)nD + 3) & ~3;   // next level starts here
-    {
+    if (K >= 4) {
       const float f = fminf(bfs_fit(nN, 65535), bfs_fit(nN * (last ? 6 : 4), tb - nb));
       out.fit = fminf(out.fit, f);
-      if (nN > 65535 || nN * (last ? 6 : 4) > tb - nb) {
-        out.C = -1;
-        out.fit = fminf(f, 0.999f);
-        return out;
-      }
+    }
+    if (nN > 65535 || nN * (last ? 6 : 4) > tb - nb) {
+      out.C = -1;
+      out.fit = fminf(out.fit, 0.999f);
+      return out;
     }
     for (int e = tid; e < nD; e += NT) {
       int mm[K];
@@ -702,7 +702,7 @@ __device__ __forceinline__ BfsOut<K> bfs_cliques(const FShared& S, FusedHdr& H, 
   __syncthreads();
   const int64_t n2 = block_scan_dpp<NT>(cnt, nr, H.red64);
   constexpr bool last = K == 2;
-  out.fit = fminf(bfs_fit(n2, 65535), bfs_fit(n2 * (last ? 6 : 4), qbytes));
+  if (K >= 4) out.fit = fminf(bfs_fit(n2, 65535), bfs_fit(n2 * (last ? 6 : 4), qbytes));
   if (n2 > 65535 || n2 * (last ? 6 : 4) > qbytes) {
     out.fit = fminf(out.fit, 0.999f);
     return out;
