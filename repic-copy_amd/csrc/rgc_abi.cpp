@@ -431,13 +431,16 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
 
   static const char* cc_names[7] = {"k4_init",     "k4_union",    "k4_compress", "k4_stats",
                                     "k4_ins_keys", "k4_comp_min", "k4_target"};
+  int max_n = 0;   // largest micrograph: LDS union-find when it fits
+  for (int m = 0; m < n_mg; ++m)
+    max_n = std::max<int>(max_n, (int)(box_off[(int64_t)(m + 1) * k] - box_off[(int64_t)m * k]));
   for (int phase = 0; phase < 7; ++phase) {
     if ((phase == 5 || phase == 6) && !get_cc) continue;
     TRY(mark(c, cc_names[phase]));
     launch_cc(s, phase, (int)N, n_mg, k, get_cc, bo, D<int32_t>(c, D_BMG), D<uint8_t>(c, D_BPICK),
               D<int64_t>(c, D_FWDOFF), D<int32_t>(c, D_EDST), D<int32_t>(c, D_PARENT),
               D<uint8_t>(c, D_HASEDGE), D<int32_t>(c, D_CSIZE), D<MgStat>(c, D_STAT),
-              D<unsigned long long>(c, D_INSKEY), D<unsigned long long>(c, D_COMPMIN));
+              D<unsigned long long>(c, D_INSKEY), D<unsigned long long>(c, D_COMPMIN), max_n);
   }
 
   CliqueArgs A;

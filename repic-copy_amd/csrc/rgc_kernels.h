@@ -170,7 +170,7 @@ void launch_cc(hipStream_t stream, int phase, int N, int n_mg, int k, int get_cc
                const int32_t* box_off, const int32_t* bmg, const uint8_t* bpick,
                const int64_t* fwd_off, const int32_t* e_dst, int32_t* parent, uint8_t* has_edge,
                int32_t* csize, MgStat* st, unsigned long long* ins_key,
-               unsigned long long* comp_min);
+               unsigned long long* comp_min, int max_n);   // max_n: largest micrograph
 // One level of the prefix expansion (rgc_cliques.hip): level-D prefixes in, children out.
 struct LevelArgs {
   int D;                     // members chosen so far (pickers 1..D)

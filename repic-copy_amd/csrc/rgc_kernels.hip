@@ -298,6 +298,52 @@ __global__ __launch_bounds__(WG) void k4_union(int N, const int64_t* __restrict_
   }
 }
 
+// Same union-find, one 1024-thread workgroup per micrograph with its parents in LDS (int32
+// per box, micrographs up to UF_LDS_MAX boxes): LDS hops instead of L2 round trips.  Writes the
+// final root of every box (global index), so k4_compress finds it in one hop.
+constexpr int UF_LDS_MAX = 39936;   // 156 KiB of int32 parents
+__device__ __forceinline__ int uf_find_l(int32_t* P, int x) {
+  for (;;) {
+    const int p = __hip_atomic_load(P + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (p == x) return x;
+    const int gp = __hip_atomic_load(P + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (gp != p) __hip_atomic_store(P + x, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    x = gp;
+  }
+}
+__global__ __launch_bounds__(1024) void k4_union_lds(int k, const int32_t* __restrict__ box_off,
+                                                     const int64_t* __restrict__ fwd_off,
+                                                     const int32_t* __restrict__ e_dst,
+                                                     int32_t* parent, uint8_t* has_edge) {
+  extern __shared__ int32_t P[];
+  const int m = blockIdx.x;
+  const int b0 = box_off[m * k], n = box_off[m * k + k] - b0;
+  for (int i = threadIdx.x; i < n; i += 1024) P[i] = i;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += 1024) {
+    const int64_t e0 = fwd_off[b0 + i], e1 = fwd_off[b0 + i + 1];
+    if (e0 == e1) continue;
+    has_edge[b0 + i] = 1;
+    for (int64_t e = e0; e < e1; ++e) {
+      const int h = e_dst[e] - b0;
+      has_edge[b0 + h] = 1;
+      int a = i, b = h;
+      for (;;) {
+        a = uf_find_l(P, a);
+        b = uf_find_l(P, b);
+        if (a == b) break;
+        if (a < b) { const int t = a; a = b; b = t; }
+        int expect = a;
+        if (__hip_atomic_compare_exchange_strong(P + a, &expect, b, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+          break;
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += 1024) parent[b0 + i] = b0 + uf_find_l(P, i);
+}
+
 __global__ __launch_bounds__(WG) void k4_compress(int N, const uint8_t* __restrict__ has_edge,
                                                   int32_t* parent, int32_t* csize) {
   const int g = blockIdx.x * WG + threadIdx.x;
@@ -677,11 +723,24 @@ void launch_cc(hipStream_t stream, int phase, int N, int n_mg, int k, int get_cc
                const int32_t* box_off, const int32_t* bmg, const uint8_t* bpick,
                const int64_t* fwd_off, const int32_t* e_dst, int32_t* parent, uint8_t* has_edge,
                int32_t* csize, MgStat* st, unsigned long long* ins_key,
-               unsigned long long* comp_min) {
+               unsigned long long* comp_min, int max_n) {
   const int nb = (N + WG - 1) / WG;
   switch (phase) {
     case 0: if (nb) RGC_LAUNCH(k4_init, nb, WG, N, parent); break;
-    case 1: if (nb) RGC_LAUNCH(k4_union, nb, WG, N, fwd_off, e_dst, parent, has_edge); break;
+    case 1:
+      if (nb && max_n <= UF_LDS_MAX) {
+        static bool attr = false;
+        if (!attr) {
+          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k4_union_lds),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+          attr = true;
+        }
+        hipLaunchKernelGGL(k4_union_lds, dim3(n_mg), dim3(1024), (size_t)max_n * 4, stream, k,
+                           box_off, fwd_off, e_dst, parent, has_edge);
+      } else if (nb) {
+        RGC_LAUNCH(k4_union, nb, WG, N, fwd_off, e_dst, parent, has_edge);
+      }
+      break;
     case 2: if (nb) RGC_LAUNCH(k4_compress, nb, WG, N, has_edge, parent, csize); break;
     case 3: RGC_LAUNCH(k4_stats, n_mg, WG, k, box_off, fwd_off, has_edge, parent, csize, st); break;
     case 4:
