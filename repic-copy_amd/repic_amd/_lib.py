@@ -213,6 +213,8 @@ class Context:
         self._pending = (keep, n_mg, k, flags)
 
     def wait(self):
+        if self._pending is None:
+            raise RGCError("rgc_wait: no submission in flight on this context")
         bo = BatchOut()
         keep, n_mg, k, flags = self._pending
         self._pending = None

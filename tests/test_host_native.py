@@ -27,7 +27,18 @@ def test_abi_exports_match_header():
     so = ctypes.CDLL(_lib.LIB_PATH)
     for name in decl:
         assert hasattr(so, name), name
-    assert _lib.abi_version() == 3
+    sys.path.insert(0, ROOT)
+    import __graft_entry__
+    assert _lib.abi_version() == __graft_entry__.header_abi_version()
+
+
+def test_graft_build_end_to_end():
+    """__graft_entry__.build() as the driver runs it: make (hipcc, gfx950) + import + ABI
+    check against include/repic_gc.h, in a fresh interpreter."""
+    import subprocess
+    r = subprocess.run([sys.executable, "-c", "import __graft_entry__ as g; g.build()"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
 
 
 def _rand_float(rng):
