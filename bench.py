@@ -64,10 +64,10 @@ def pipeline_bytes(N, E, C, k):
     return 28 * N + 32 * E + C * (20 * k + 12)
 
 
-def pmc_traffic(kernel, config):
-    """HBM bytes per launch of ``kernel`` from the newest profiles/*_traffic.json written by
-    tools/pmc_traffic.py for THIS library build (sha256 must match) on THIS workload
-    (config; files without one were C2 runs), else None."""
+def pmc_record(config):
+    """The newest profiles/*_traffic.json written by tools/pmc_traffic.py for THIS library
+    build (sha256 must match) on THIS workload (config; files without one were C2 runs), as
+    (record, file name), else (None, None)."""
     import glob
     import hashlib
     from repic_amd import _lib
@@ -77,10 +77,42 @@ def pmc_traffic(kernel, config):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if (d.get("lib_sha256") == sha and d.get("config", "C2") == config
-                and kernel in d.get("kernels", {})):
-            return d["kernels"][kernel]["traffic"], os.path.basename(f)
+        if d.get("lib_sha256") == sha and d.get("config", "C2") == config:
+            return d, os.path.basename(f)
     return None, None
+
+
+def roofline_evidence(rec, kernel, alg_bytes, kernel_ms):
+    """(traffic bytes per launch/step, measured HBM fraction, limiter text) from the config's
+    committed counters; the limiter names what the counters show, not a fixed claim."""
+    if rec is None:
+        return None, None, ("unmeasured for this library build: no profiles/*_traffic.json "
+                            "with its sha256 for this config")
+    if kernel == "k_fused":
+        k = rec.get("kernels", {}).get("k_fused")
+        if k is None:
+            return None, None, "no k_fused counters in the matching PMC file"
+        traffic, dv = k["traffic"], k.get("derived", {})
+    else:
+        traffic, dv = rec.get("step_traffic"), {}
+        if traffic is None:
+            return None, None, "no per-step traffic in the matching PMC file"
+    hbm = traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+    parts = [f"measured HBM traffic {traffic / 1e6:.0f} MB/launch = {traffic / alg_bytes:.2f}x "
+             f"B_alg, {hbm * HBM_PEAK_GBS / 1e3:.2f} TB/s = {100 * hbm:.0f}% of peak"]
+    if "valu_busy" in dv:
+        parts.append(f"VALU busy {100 * dv['valu_busy']:.0f}%")
+    if "wait_any" in dv:
+        parts.append(f"waves stalled {100 * dv['wait_any']:.0f}% of resident time")
+    if "waves_per_cu" in dv:
+        parts.append(f"{dv['waves_per_cu']:.1f} resident waves/CU")
+    if "lane_eff" in dv:
+        parts.append(f"VALU lane efficiency {100 * dv['lane_eff']:.0f}%")
+    bound = ("VALU issue" if dv.get("valu_busy", 0) > 0.6 and hbm < 0.5 else
+             "HBM bandwidth" if hbm >= 0.5 else "latency (neither VALU nor HBM saturated)")
+    if not dv:
+        bound = "HBM bandwidth" if hbm >= 0.5 else "not HBM bandwidth (issue counters not collected)"
+    return traffic, hbm, f"{bound}: " + "; ".join(parts)
 
 
 def _cpu_model():
@@ -122,9 +154,54 @@ def _oracle_worker(cfg_kw, start, n_max, budget_s):
     return _oracle_loop(cfg, mgs, budget_s)
 
 
-def cpu_baseline(cfg, mgs, budget_s=12.0, procs=None):
+def _pair_loop_sample(cfg, mg, budget_s):
+    """BASELINE.md §3 for C5 (one micrograph takes far longer than any bench budget): time the
+    oracle's faithful per-pair loop (get_cliques.py:59-69, >= 97 % of the reference's time on
+    C1) over the first rows of every picker pair's outer loop for ``budget_s`` in all, and
+    extrapolate each pair to its full outer loop.  Later stages (graph, cliques, epilogue) are
+    not timed, so the returned micrograph time UNDERSTATES the reference's (the CPU rate is an
+    upper bound)."""
+    import itertools
+
+    from oracle import cpu_ref
+    P = []
+    nid = 0
+    for (x, y, s) in mg:
+        P.append([(float(a), float(b), float(c), nid + i)
+                  for i, (a, b, c) in enumerate(zip(x.tolist(), y.tolist(), s.tolist()))])
+        nid += len(x)
+    pairs = list(itertools.combinations(range(cfg.k), 2))
+    per = budget_s / len(pairs)
+    est, rows_done, rows_all = 0.0, 0, 0
+    for (j, l) in pairs:
+        t0 = time.perf_counter()
+        r = 0
+        step = max(1, len(P[j]) // 200)
+        while r < len(P[j]) and time.perf_counter() - t0 < per:
+            cpu_ref.edges_faithful(P[j][r:r + step], P[l], cfg.box)
+            r += step
+        dt = time.perf_counter() - t0
+        r = min(r, len(P[j]))
+        est += dt * len(P[j]) / max(r, 1)
+        rows_done += r
+        rows_all += len(P[j])
+    return est, rows_done, rows_all
+
+
+def cpu_baseline(cfg, mgs, budget_s=12.0, procs=None, config=None):
     """1 process (the reference is single-threaded) and P processes on disjoint micrograph
-    shards, P = this host's CPU share capped at 16 (the GPU box's share)."""
+    shards, P = this host's CPU share capped at 16 (the GPU box's share).
+    C5 (a micrograph takes tens of minutes): one micrograph's pair loop, sampled and
+    extrapolated (_pair_loop_sample), 1 process only."""
+    if config == "C5":
+        est, done, tot = _pair_loop_sample(cfg, mgs[0], budget_s)
+        return {"value": 1.0 / est, "unit": "micrographs/s", "cores": 1, "kind": "port",
+                "sample": f"1 micrograph: faithful per-pair loop (get_cliques.py:59-69) over "
+                          f"{done} of {tot} outer-loop boxes across all {cfg.k * (cfg.k - 1) // 2} "
+                          f"picker pairs in ~{budget_s:.0f} s, extrapolated to the whole pair "
+                          f"loop ({est:.0f} s per micrograph); graph/clique/epilogue stages not "
+                          f"timed, so this rate is an upper bound on the reference's",
+                "cpu_model": _cpu_model()}
     n, dt = _oracle_loop(cfg, mgs, budget_s)
     out = {"value": n / dt, "unit": "micrographs/s", "cores": 1, "kind": "port",
            "sample": f"{n} micrographs of this workload, oracle faithful per-pair loop "
@@ -359,7 +436,9 @@ def main():
         dom_bytes = pipe
         dom_ms = dev_ms
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic("k_fused" if dom == "k_fused" else dom, args.config)
+    rec, traffic_src = pmc_record(args.config)
+    traffic, hbm_frac, limiter = roofline_evidence(rec, "k_fused" if dom == "k_fused" else "route",
+                                                   dom_bytes, dom_ms)
     out = {
         "metric": "micrographs/sec (get_cliques, whole node) at 1/2/4/8 MI355X; % HBM roofline",
         "value": value, "unit": "micrographs/s", "n_gpus": world, "steps": steps,
@@ -376,11 +455,11 @@ def main():
         "totals": {"micrographs": tot_mg, "edges": tot_e, "cliques": tot_c},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
                      # priced against HBM (no contraction: no MFMA roofline applies); the
-                     # PMC counters show the limiter is not HBM bandwidth
-                     "limiter": "LDS latency / VALU issue on a data-dependent graph walk "
-                                "(PMC: HBM traffic 0.26-0.38x B_alg, SQ_WAIT_ANY ~56%)",
+                     # limiter is derived from this build's committed PMC counters
+                     "limiter": limiter,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": traffic_src,
+                     "hbm_frac_measured": hbm_frac,
                      "alg_bytes_per_step": dom_bytes, "alg_bytes_formula":
                          "SURVEY.md 8(d): 28 N + 32 E + C (20 k + 12)",
                      "compulsory_bytes_per_step": fused_compulsory_bytes(N, C, cfg.k, V, n_mg),
@@ -392,7 +471,7 @@ def main():
         "gen_s": t_gen,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cfg, mgs, args.cpu_budget)
+        out["cpu_baseline"] = cpu_baseline(cfg, mgs, args.cpu_budget, config=args.config)
     if rank == 0:
         print(json.dumps(out), flush=True)
     for c in ctxs:

@@ -121,7 +121,9 @@ int rgc_run(rgc_ctx* ctx, const rgc_batch_in* in, rgc_batch_out* out);
  * | RGC_F_DEVICE_META, device outputs) runs while the caller continues, so with two contexts
  * on one stream the host prepares and launches batch i+1 while the device runs batch i; any
  * other batch (or one whose micrographs need a second pass) runs through rgc_run's general
- * path.  Outputs stay valid until the next submit/run on the same context. */
+ * path.  Outputs stay valid until the next submit/run on the same context.  While a submitted
+ * run awaits rgc_wait, rgc_submit, rgc_run, rgc_score_pairs and rgc_ilp_solve on the same
+ * context fail (negative return, rgc_last_error says why). */
 int rgc_submit(rgc_ctx* ctx, const rgc_batch_in* in);
 int rgc_wait(rgc_ctx* ctx, rgc_batch_out* out);
 /* Per-kernel device milliseconds of the last rgc_run with RGC_F_TIMING; returns the count. */

@@ -1151,6 +1151,7 @@ void rgc_ctx_destroy(rgc_ctx* c) {
 
 int rgc_run(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   if (!c || !in || !out) return fail("null argument");
+  if (c->pend) return fail("rgc_run: a submitted run awaits rgc_wait on this context");
   HIPCHK(hipSetDevice(c->device));
   return run_impl(c, in, out);
 }
@@ -1203,6 +1204,7 @@ int64_t rgc_last_edges(rgc_ctx* c, const int32_t** u, const int32_t** v, const d
 
 int rgc_score_pairs(rgc_ctx* c, const rgc_score_in* in, int64_t* counts) {
   if (!c || !in || !counts) return fail("null argument");
+  if (c->pend) return fail("rgc_score_pairs: a submitted run awaits rgc_wait on this context");
   HIPCHK(hipSetDevice(c->device));
   const int64_t np = in->n_pairs;
   if (np < 0 || np > INT32_MAX) return fail("n_pairs out of range");
@@ -1295,6 +1297,7 @@ int rgc_score_pairs(rgc_ctx* c, const rgc_score_in* in, int64_t* counts) {
 
 int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) {
   if (!c || !in || !x || !exact) return fail("null argument");
+  if (c->pend) return fail("rgc_ilp_solve: a submitted run awaits rgc_wait on this context");
   HIPCHK(hipSetDevice(c->device));
   const int64_t nc = in->n_cols, nr = in->n_rows;
   if (nc < 0 || nc >= INT32_MAX || nr < 0 || nr >= INT32_MAX) return fail("n_cols / n_rows out of range");

@@ -1613,13 +1613,10 @@ void k_fused(FusedArgs A) {
 
 template <int K, bool W, int NT>
 static int launch_fused_t(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArgs& A) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused<K, W, NT>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return (int)e;
-    attr_set = true;
-  }
+  static std::atomic<uint64_t> attr_set{0};   // per device
+  const hipError_t e = set_dyn_lds_once(attr_set, reinterpret_cast<const void*>(&k_fused<K, W, NT>),
+                                        160 * 1024);
+  if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL((k_fused<K, W, NT>), dim3(n_blocks), dim3(NT), lds_bytes, stream, A);
   return (int)hipGetLastError();
 }

@@ -3,7 +3,23 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 namespace rgc {
+
+// Raise a kernel's dynamic-LDS limit to `bytes` on the CURRENT device, once per (kernel,
+// device): `done` is the kernel's own bitmask of devices already set (thread-safe; a racing
+// second setter only repeats an idempotent call).  Returns the HIP error of the call.
+inline hipError_t set_dyn_lds_once(std::atomic<uint64_t>& done, const void* fn, int bytes) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  const uint64_t bit = dev < 64 ? (1ULL << dev) : 0;
+  if (bit && (done.load(std::memory_order_acquire) & bit)) return hipSuccess;
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess && bit) done.fetch_or(bit, std::memory_order_acq_rel);
+  return e;
+}
 
 constexpr int MAX_K = 8;            // largest picker count with a compiled clique kernel
 constexpr int CELL_CAP = 8192;      // LDS counters per micrograph grid (k1_bin)

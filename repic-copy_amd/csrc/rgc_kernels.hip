@@ -728,13 +728,12 @@ void launch_cc(hipStream_t stream, int phase, int N, int n_mg, int k, int get_cc
   switch (phase) {
     case 0: if (nb) RGC_LAUNCH(k4_init, nb, WG, N, parent); break;
     case 1:
-      if (nb && max_n <= UF_LDS_MAX) {
-        static bool attr = false;
-        if (!attr) {
-          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k4_union_lds),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-          attr = true;
-        }
+      // LDS union-find needs the 160 KiB dynamic-LDS limit on this device; if it cannot be
+      // set, the global-memory union-find runs instead
+      static std::atomic<uint64_t> lds_attr{0};
+      if (nb && max_n <= UF_LDS_MAX &&
+          set_dyn_lds_once(lds_attr, reinterpret_cast<const void*>(&k4_union_lds), 160 * 1024) ==
+              hipSuccess) {
         hipLaunchKernelGGL(k4_union_lds, dim3(n_mg), dim3(1024), (size_t)max_n * 4, stream, k,
                            box_off, fwd_off, e_dst, parent, has_edge);
       } else if (nb) {

@@ -1,0 +1,46 @@
+"""CPU tests of bench.py's host-side reporting: the roofline limiter / measured HBM fraction
+derived from a PMC record, and the C5 sampled CPU baseline."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def test_roofline_evidence_from_counters():
+    rec = {"kernels": {"k_fused": {"traffic": 346e6, "derived": {
+        "valu_busy": 0.867, "wait_any": 0.541, "waves_per_cu": 26.0, "lane_eff": 0.62}}}}
+    traffic, hbm, lim = bench.roofline_evidence(rec, "k_fused", 995e6, 0.54)
+    assert traffic == 346e6
+    assert hbm == pytest.approx(346e6 / 0.54e-3 / 8e12)
+    assert lim.startswith("VALU issue:")
+    for frag in ("0.35x B_alg", "VALU busy 87%", "stalled 54%", "lane efficiency 62%"):
+        assert frag in lim, (frag, lim)
+    # an HBM-saturating kernel is labelled as such
+    rec2 = {"kernels": {"k_fused": {"traffic": 4.4e9, "derived": {"valu_busy": 0.3}}}}
+    assert bench.roofline_evidence(rec2, "k_fused", 4e9, 1.0)[2].startswith("HBM bandwidth")
+    # multi-kernel route: per-step traffic over the route's device time
+    rec3 = {"step_traffic": 2e9, "kernels": {}}
+    t, h, lim3 = bench.roofline_evidence(rec3, "route", 8e9, 8.0)
+    assert t == 2e9 and h == pytest.approx(2e9 / 8e-3 / 8e12)
+    # no matching file: said so, no numbers
+    t, h, lim4 = bench.roofline_evidence(None, "k_fused", 1.0, 1.0)
+    assert t is None and h is None and "unmeasured" in lim4
+
+
+def test_c5_cpu_baseline_is_sampled_and_bounded():
+    sys.path.insert(0, os.path.join(ROOT, "repic-copy_amd"))
+    import time
+
+    from repic_amd import synth
+    cfg = synth.SynthConfig(**synth.CONFIGS["C5"], seed=0)
+    mgs = synth.batch(cfg, 1)
+    t0 = time.perf_counter()
+    cb = bench.cpu_baseline(cfg, mgs, budget_s=1.5, procs=1, config="C5")
+    assert time.perf_counter() - t0 < 10
+    assert cb["cores"] == 1 and cb["kind"] == "port" and 0 < cb["value"] < 0.1
+    assert "extrapolated" in cb["sample"] and "upper bound" in cb["sample"]

@@ -395,6 +395,24 @@ def _submit_wait_check():
                  t[2].data_ptr(), fl | _lib.F_DEVICE_INPUTS | _lib.F_TIMING,
                  dev_meta=(t[3].data_ptr(), t[4].data_ptr()))
 
+    # one run in flight per context: wait() with nothing pending raises, and while a submit is
+    # pending, run / submit on the same context are refused (its buffers are in use)
+    try:
+        ctxs[0].wait()
+        raise AssertionError("wait() without a submission did not raise")
+    except _lib.RGCError:
+        pass
+    submit(ctxs[0], 0)
+    for call in (lambda: submit(ctxs[0], 1),
+                 lambda: ctxs[0].run(b1.n_mg, 3, 180, b1.box_off, b1.id_base, b1.x, b1.y,
+                                     b1.score, fl | _lib.F_HOST_OUTPUTS)):
+        try:
+            call()
+            raise AssertionError("call on a busy context did not raise")
+        except _lib.RGCError as e:
+            assert "awaits rgc_wait" in str(e)
+    ctxs[0].wait()
+
     order = [0, 1, 2, 0, 2, 1]
     submit(ctxs[0], order[0])
     for j, i in enumerate(order):

@@ -1,28 +1,34 @@
 #!/bin/bash
-# PMC passes over a short bench run: SQ issue/stall counters, HBM traffic (FETCH_SIZE and
-# WRITE_SIZE in separate passes, per MI355X_MICROARCH.md), GRBM clock.  One counter group per
-# rocprofv3 run, each under its own SIGKILL time limit; the first failure ends the script.
-#   gpurun --timeout 900 -- bash tools/gpu_pmc.sh TAG [bench args...]
+# PMC passes over a short bench run of one config: SQ issue/stall counters, VALU lane cycles,
+# HBM traffic (FETCH_SIZE and WRITE_SIZE in separate passes, per MI355X_MICROARCH.md), GRBM
+# clock.  One counter group per rocprofv3 run, each under its own SIGKILL time limit; the first
+# failure ends the script.  tools/pmc_traffic.py folds them into OUT/traffic.json (bench.py
+# reads it from profiles/ when the library sha256 and the config match).
+#   gpurun --timeout 900 -- bash tools/gpu_pmc.sh TAG [CONFIG] [N_MG]
 set -e -o pipefail
-TAG=${1:-pmc}
-shift || true
+TAG=${1:-pmc}; CFG=${2:-C2}; NMG=${3:-}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH=(python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 "$@")
+STEPS=3; WARM=1
+BENCH=(python3 bench.py --no-cpu-baseline --steps $STEPS --warmup $WARM --config "$CFG")
+if [ -n "$NMG" ]; then BENCH+=(--n_mg "$NMG"); fi
+KSUB=k_fused
+if [ "$CFG" = "C5" ]; then KSUB=rgc::; fi
 pass() {  # name counters...
   local name=$1
   shift
   echo "== pass $name: $*"
-  timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- \
+  timeout -s KILL 150 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- \
     "${BENCH[@]}" > "$OUT/$name.json" 2> "$OUT/$name.err" || { tail -20 "$OUT/$name.err"; exit 1; }
   find "$OUT/$name" -name '*counter_collection.csv' -exec cp {} "$OUT/$name.csv" \;
-  python3 tools/pmc_summary.py k_fused "$OUT/$name.csv"
+  python3 tools/pmc_summary.py "$KSUB" "$OUT/$name.csv"
 }
 pass sqa SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS
 pass sqb SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH
+pass lane SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU
 pass grbm GRBM_GUI_ACTIVE GRBM_COUNT
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE
-python3 tools/pmc_traffic.py "$OUT/fetch.csv" "$OUT/write.csv" repic-copy_amd/repic_amd/librepic_gc.so "$OUT/traffic.json" "$(python3 -c 'import sys;a=sys.argv[1:];print(a[a.index("--config")+1] if "--config" in a else "C2")' "$@")"
+python3 tools/pmc_traffic.py "$OUT" repic-copy_amd/repic_amd/librepic_gc.so "$OUT/traffic.json" "$CFG" $((STEPS + WARM))
 echo "== done"
