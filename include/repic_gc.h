@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RGC_ABI_VERSION 3
+#define RGC_ABI_VERSION 4
 
 /* flags for rgc_batch_in.flags */
 #define RGC_F_GET_CC         1u  /* --get_cc   (get_cliques.py:151-156) */
@@ -154,9 +154,19 @@ int rgc_score_pairs(rgc_ctx* ctx, const rgc_score_in* in, int64_t* counts);
 /* run_ilp (repic/commands/run_ilp.py:50-63): maximise w.x over binary x subject to A x <= 1,
  * exactly, for a batch of micrographs at once (rows are global box ids: micrographs never
  * share a row).  A is given in CSC form.  x[c] = 1 for the chosen columns (cliques);
- * exact[c] = 1 when column c's conflict component was solved to proven optimality (0: the
- * component hit node_limit and x holds the best packing found).  RGC_F_TIMING records the
- * stages in rgc_kernel_times. */
+ * exact[c] is the status of column c's conflict component:
+ *   RGC_ILP_OPTIMAL  (1) proven optimal by the branch and bound;
+ *   RGC_ILP_GAP_OK   (2) not searched to the end (more than 4096 cliques, or node_limit hit),
+ *                        but a Lagrangian dual bound certifies x within a relative gap of 1e-4,
+ *                        the default MIPGap at which Gurobi reports a model optimal;
+ *   RGC_ILP_NODE_LIMIT (0) node_limit hit, x is the best packing found, gap above 1e-4;
+ *   RGC_ILP_HEURISTIC (3) too large to search, x is a greedy + swap local-search packing,
+ *                        gap above 1e-4.
+ * RGC_F_TIMING records the stages in rgc_kernel_times. */
+#define RGC_ILP_NODE_LIMIT 0
+#define RGC_ILP_OPTIMAL 1
+#define RGC_ILP_GAP_OK 2
+#define RGC_ILP_HEURISTIC 3
 typedef struct rgc_ilp_in {
   int64_t n_cols;          /* cliques */
   int64_t n_rows;          /* boxes */

@@ -17,10 +17,15 @@
 // also correctly rounded).  Files with any byte >= 0x80 are returned as FALLBACK so the
 // host parses them with Python's own str/float semantics.
 #include <atomic>
+#include <cerrno>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <cstdint>
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <locale.h>
 #include <string>
 #include <thread>
@@ -73,9 +78,67 @@ locale_t c_locale() {
   return loc;
 }
 
+// Exact powers of ten 10^0 .. 10^27 in x87 extended precision (5^27 < 2^64: every one is exact)
+struct Pow10L {
+  long double v[28];
+  Pow10L() {
+    long double t = 1.0L;
+    for (int i = 0; i < 28; ++i, t *= 10.0L) v[i] = t;
+  }
+};
+const Pow10L kPow10L;
+
+// Fast path of Python float() for the tokens BOX files are made of: [sign] digits [. digits]
+// with at most 19 significant digits and 27 fraction digits (no exponent, no underscores).
+// m / 10^f is computed in x87 extended precision (64-bit significand: m and 10^f are exact, so
+// the quotient is correctly rounded to 64 bits) and then rounded to double.  That double
+// rounding equals the correctly rounded result unless the 64-bit quotient lies within one unit
+// of a double rounding midpoint (its low 11 significand bits 0x3FF..0x401): those, and every
+// other shape, return false and take the strtod path.
+inline bool fast_decimal(const char* p, size_t n, double* out) {
+  size_t i = 0;
+  bool neg = false;
+  if (i < n && (p[i] == '+' || p[i] == '-')) neg = p[i++] == '-';
+  uint64_t m = 0;
+  int digits = 0, frac = 0;
+  bool any = false, dot = false;
+  for (; i < n; ++i) {
+    const unsigned char c = (unsigned char)p[i];
+    if (c >= '0' && c <= '9') {
+      any = true;
+      if (digits > 0 || c != '0') {
+        if (++digits > 19) return false;
+      }
+      m = m * 10 + (c - '0');
+      if (dot && ++frac > 27) return false;
+    } else if (c == '.' && !dot) {
+      dot = true;
+    } else {
+      return false;   // exponent, underscore, letters: strtod path (or not a float at all)
+    }
+  }
+  if (!any) return false;
+  if (frac == 0 && m < (1ULL << 53)) {
+    const double d = (double)m;
+    *out = neg ? -d : d;
+    return true;
+  }
+  const long double q = (long double)m / kPow10L.v[frac];
+  if (frac > 0) {
+    uint64_t sig;
+    std::memcpy(&sig, &q, sizeof(sig));   // x87 extended: 64-bit significand in the low bytes
+    const uint32_t low = (uint32_t)(sig & 0x7FF);
+    if (low >= 0x3FF && low <= 0x401) return false;
+  }
+  const double d = (double)q;
+  *out = neg ? -d : d;
+  return true;
+}
+
 // Python float(token) for an ASCII token without whitespace.
 bool py_float(const char* p, size_t n, double* out) {
   if (n == 0) return false;
+  if (fast_decimal(p, n, out)) return true;
   size_t i = 0;
   bool neg = false;
   if (p[0] == '+' || p[0] == '-') {
@@ -141,35 +204,72 @@ inline int split5(const char* b, const char* e, Tok* t) {
   return cnt;
 }
 
+struct Row {
+  Tok x, y, w;
+};
+
 void parse_one(const char* path, FileResult& R) {
-  FILE* f = std::fopen(path, "rb");
-  if (!f) {
+  const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) {
     R.status = RGC_PARSE_OSERROR;
     return;
   }
-  std::string data;
-  char chunk[1 << 16];
-  size_t got;
-  while ((got = std::fread(chunk, 1, sizeof(chunk), f)) > 0) data.append(chunk, got);
-  const bool err = std::ferror(f);
-  std::fclose(f);
+  // one read of the whole file (sized by fstat; grown if the file is longer than reported)
+  thread_local std::string data;
+  struct stat stt;
+  size_t cap = (::fstat(fd, &stt) == 0 && stt.st_size > 0) ? (size_t)stt.st_size + 1 : 1 << 16;
+  data.resize(cap);
+  size_t len = 0;
+  bool err = false;
+  for (;;) {
+    if (len == data.size()) data.resize(2 * data.size());
+    const ssize_t got = ::read(fd, &data[len], data.size() - len);
+    if (got < 0) {
+      if (errno == EINTR) continue;
+      err = true;
+      break;
+    }
+    if (got == 0) break;
+    len += (size_t)got;
+  }
+  ::close(fd);
   if (err) {
     R.status = RGC_PARSE_OSERROR;
     return;
   }
-  for (unsigned char ch : data)
-    if (ch >= 0x80) {
+  data.resize(len);
+  {
+    // any byte >= 0x80 (8 bytes per step)
+    const char* q = data.data();
+    const size_t nb = data.size();
+    uint64_t acc = 0;
+    size_t i = 0;
+    for (; i + 8 <= nb; i += 8) {
+      uint64_t w;
+      std::memcpy(&w, q + i, 8);
+      acc |= w;
+    }
+    for (; i < nb; ++i) acc |= (unsigned char)q[i];
+    if (acc & 0x8080808080808080ULL) {
       R.status = RGC_PARSE_FALLBACK;
       return;
     }
+  }
   const char* p = data.data();
   const char* end = p + data.size();
-  // universal-newline line iterator
+  // universal-newline line iterator (memchr for '\n' when the file has no '\r')
+  const bool has_cr = std::memchr(p, '\r', data.size()) != nullptr;
   auto next_line = [&](const char*& cur, const char*& lb, const char*& le) -> bool {
     if (cur >= end) return false;
     lb = cur;
-    const char* q = cur;
-    while (q < end && *q != '\n' && *q != '\r') ++q;
+    const char* q;
+    if (!has_cr) {
+      q = static_cast<const char*>(std::memchr(cur, '\n', (size_t)(end - cur)));
+      if (!q) q = end;
+    } else {
+      q = cur;
+      while (q < end && *q != '\n' && *q != '\r') ++q;
+    }
     le = q;
     if (q < end) {
       if (*q == '\r' && q + 1 < end && q[1] == '\n') q += 2;
@@ -188,10 +288,8 @@ void parse_one(const char* path, FileResult& R) {
     return;
   }
   if (py_float(t[0].p, t[0].n, &v)) cur = p;  // f.seek(0)
-  struct Row {
-    Tok x, y, w;
-  };
-  std::vector<Row> rows;
+  thread_local std::vector<Row> rows;
+  rows.clear();
   int min_tok = 1 << 30;
   while (next_line(cur, lb, le)) {
     const int c = split5(lb, le, t);

@@ -67,7 +67,8 @@ enum DevBufId {
   // run_ilp set packing
   D_IL_CPTR, D_IL_ROW, D_IL_W, D_IL_REP, D_IL_PAR, D_IL_ROOT, D_IL_CSIZE, D_IL_RCNT, D_IL_RCUR,
   D_IL_RPTR, D_IL_RCOLS, D_IL_CID, D_IL_CN, D_IL_COFF, D_IL_CCUR, D_IL_MEM, D_IL_LOC, D_IL_SCR,
-  D_IL_BIG, D_IL_NBIG, D_IL_WSCR, D_IL_X, D_IL_EX, D_IL_RLOC,
+  D_IL_BIG, D_IL_NBIG, D_IL_WSCR, D_IL_X, D_IL_EX, D_IL_RLOC, D_IL_CERT, D_IL_KEY, D_IL_ST,
+  D_IL_RMAX, D_IL_OWN, D_IL_LAM, D_IL_GRAD, D_IL_CS, D_IL_CNT,
   D_COUNT
 };
 enum HostBufId {
@@ -108,8 +109,8 @@ struct FusedPlan {
 // Workgroups per CU the VGPRs of the nt-thread kernel allow (nt / 64 waves per workgroup over
 // 4 SIMDs of 512 VGPRs, at most 8 waves per SIMD).
 static int vgpr_wg_cap(int k, bool wide, int nt) {
-  static int cache[2][MAX_K + 1][3] = {};
-  int& v = cache[wide][k][nt == 512 ? 0 : (nt == 768 ? 1 : 2)];
+  static int cache[2][MAX_K + 1][4] = {};
+  int& v = cache[wide][k][std::min(3, std::max(0, nt / 256 - 1))];
   if (!v) {
     const int r = fused_vgprs(k, wide, nt);
     const int waves = r > 0 ? std::min(8, 512 / (((r + 7) / 8) * 8)) : 0;
@@ -133,7 +134,7 @@ static bool plan_fused(int k, bool wide, int nmax, int max_wg, FusedPlan* p) {
     return e ? atoi(e) : 0;
   }();
   int w = 0, nt = 512, best_waves = 0;
-  for (int cand : {512, 768, 1024}) {
+  for (int cand : {256, 512, 768, 1024}) {
     if (!fused_nt_ok(k, cand) || (diag_nt && fused_nt_ok(k, diag_nt) && cand != diag_nt)) continue;
     const int wc = std::min(std::min(max_wg, vgpr_wg_cap(k, wide, cand)), LDS_BLOCKS / need);
     if (wc < 1) continue;
@@ -1413,6 +1414,46 @@ int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) 
     TRY(mark(c, "k_ilp_wave"));
     rgc::launch_ilp(s, 4, A, n_big, n_waves);
   }
+  // certification of the components the branch and bound left unproven (rgc_ilp.hip)
+  TRY(ensure_dev(c, D_IL_CERT, ncomp + 1));
+  TRY(ensure_dev(c, D_IL_KEY, nc * 8));
+  TRY(ensure_dev(c, D_IL_ST, nc));
+  TRY(ensure_dev(c, D_IL_RMAX, nr * 8 + 8));
+  TRY(ensure_dev(c, D_IL_OWN, nr * 4 + 4));
+  TRY(ensure_dev(c, D_IL_LAM, nr * 8 + 8));
+  TRY(ensure_dev(c, D_IL_GRAD, nr * 8 + 8));
+  TRY(ensure_dev(c, D_IL_CS, (ncomp + 1) * 8 * 8));
+  TRY(ensure_dev(c, D_IL_CNT, 16));
+  A.cert = D<uint8_t>(c, D_IL_CERT);
+  A.key = D<uint64_t>(c, D_IL_KEY);
+  A.st = D<uint8_t>(c, D_IL_ST);
+  A.rmax = D<uint64_t>(c, D_IL_RMAX);
+  A.owner = D<int32_t>(c, D_IL_OWN);
+  A.lam = D<double>(c, D_IL_LAM);
+  A.grad = D<double>(c, D_IL_GRAD);
+  A.cs = D<double>(c, D_IL_CS);
+  A.count = D<unsigned int>(c, D_IL_CNT);
+  TRY(mark(c, "k_ilp_cert"));
+  rgc::launch_ilp_cert(s, 0, A);
+  // rounds until a pass changes nothing (each round settles at least the heaviest undecided
+  // clique / makes at least one improving swap, so both terminate); counters read every 4
+  auto rounds = [&](int phase, int cap) -> int {
+    for (int it = 0; it < cap; it += 4) {
+      HIPCHK(hipMemsetAsync(A.count, 0, 4, s));
+      for (int j = 0; j < 4; ++j) rgc::launch_ilp_cert(s, phase, A);
+      HIPCHK(hipMemcpyAsync(H<int64_t>(c, H_TOTAL) + 3, A.count, 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      if (*reinterpret_cast<uint32_t*>(H<int64_t>(c, H_TOTAL) + 3) == 0) break;
+    }
+    return 0;
+  };
+  TRY(rounds(1, 1 << 20));
+  TRY(rounds(2, 1 << 16));
+  rgc::launch_ilp_cert(s, 3, A);
+  // projected subgradient iterations of the Lagrangian bound (per component Polyak steps,
+  // halved after 8 iterations without progress: 300 halve mu up to ~37 times)
+  for (int it = 0; it < 300; ++it) rgc::launch_ilp_cert(s, 4, A);
+  rgc::launch_ilp_cert(s, 5, A);
   TRY(mark(c, "d2h_x"));
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(x, A.x, nc, hipMemcpyDeviceToHost, s));

@@ -31,8 +31,10 @@ namespace rgc {
 
 constexpr int MAXW = 16;            // reduction slots: up to 1024-thread workgroups
 // Workgroup sizes compiled: 512 for every k; 768 / 1024 threads (12 / 16 waves) for k <= 5,
-// launched when LDS allows few workgroups per CU but VGPRs allow more waves (rgc_abi.cpp).
-constexpr int RB = 2;               // boxes per thread kept in registers from P0 to P1
+// launched when LDS allows few workgroups per CU but VGPRs allow more waves (rgc_abi.cpp);
+// 256 threads for k <= 3 (fewer per-wave fixed costs per micrograph, fewer resident waves).
+// boxes per thread kept in registers from P0 to P1: 2 (4 with 256-thread workgroups)
+constexpr int fused_rb(int nt) { return nt <= 256 ? 4 : 2; }
 
 struct FusedHdr {
   // reduction scratch: the single-value reductions alias the 4-way one (every reduction
@@ -855,6 +857,34 @@ __device__ __forceinline__ int pairs_count_int(const Stencil& st, const FShared&
   uint32_t mask = 0;
   int cnt = 0, kk = 0;
   const float ax = (float)st.a.x, ay = (float)st.a.y;
+#ifdef RGC_X_P2A
+  // every stencil range of every higher picker first (one batch of LDS reads), then one
+  // non-unrolled candidate loop per range
+  constexpr int NR = 3 * (K - 1);
+  int lo[NR], hi[NR];
+#pragma unroll
+  for (int qi = 0; qi < K - 1; ++qi)
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      int l = 0, h = 0;
+      if (qi + 1 > st.p) stencil_range(st, S, H, qi + 1, d - 1, l, h);
+      lo[qi * 3 + d] = l;
+      hi[qi * 3 + d] = h;
+    }
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+#pragma unroll 1
+    for (int t = lo[r]; t < hi[r]; ++t, ++kk) {
+      const float2 bf = reinterpret_cast<const float2*>(S.sxy)[t];
+      const float xo = fmaxf(Bf - fabsf(ax - bf.x), 0.0f);
+      const float yo = fmaxf(Bf - fabsf(ay - bf.y), 0.0f);
+      if (xo * yo > Tf) {
+        ++cnt;
+        mask |= (kk < 32) ? (1u << kk) : 0u;
+      }
+    }
+  }
+#else
   for (int q = st.p + 1; q < K; ++q) {
 #pragma unroll
     for (int d = -1; d <= 1; ++d) {
@@ -871,6 +901,7 @@ __device__ __forceinline__ int pairs_count_int(const Stencil& st, const FShared&
       }
     }
   }
+#endif
   *mask_out = mask;
   return cnt;
 }
@@ -934,7 +965,7 @@ __device__ __forceinline__ void put_stats(const FusedArgs& A, int m, int status,
 constexpr int fused_waves_per_eu(int, int) { return 1; }
 #else
 constexpr int fused_waves_per_eu(int k, int nt) {
-  return nt == 1024 ? 4 : (nt == 768 ? 6 : (k <= 3 ? 8 : 1));
+  return nt == 1024 ? 4 : (nt == 768 ? 6 : (nt == 256 ? 4 : (k <= 3 ? 8 : 1)));
 }
 #endif
 
@@ -1007,6 +1038,7 @@ void k_fused(FusedArgs A) {
 
   // ---- P0: load coordinates (the first RB boxes of each thread stay in registers for P1),
   // bounding box (one combined workgroup reduction)
+  constexpr int RB = fused_rb(NT);
   double rx[RB], ry[RB];
 #pragma unroll
   for (int j = 0; j < RB; ++j) {
@@ -1632,11 +1664,14 @@ static int fused_vgprs_t() {
 // workgroup sizes compiled for k (fused_nt_ok) and their dispatch
 bool fused_nt_ok(int k, int nt) {
   if (k < 2 || k > 8) return false;
-  return nt == 512 || ((nt == 768 || nt == 1024) && k <= 5);
+  return nt == 512 || ((nt == 768 || nt == 1024) && k <= 5) || (nt == 256 && k <= 3);
 }
 
 template <int K, bool W>
 static int fused_vgprs_k(int nt) {
+  if constexpr (K <= 3) {
+    if (nt == 256) return fused_vgprs_t<K, W, 256>();
+  }
   if constexpr (K <= 5) {
     if (nt == 768) return fused_vgprs_t<K, W, 768>();
     if (nt == 1024) return fused_vgprs_t<K, W, 1024>();
@@ -1647,6 +1682,9 @@ static int fused_vgprs_k(int nt) {
 template <int K, bool W>
 static int launch_fused_k(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArgs& A,
                           int nt) {
+  if constexpr (K <= 3) {
+    if (nt == 256) return launch_fused_t<K, W, 256>(stream, n_blocks, lds_bytes, A);
+  }
   if constexpr (K <= 5) {
     if (nt == 768) return launch_fused_t<K, W, 768>(stream, n_blocks, lds_bytes, A);
     if (nt == 1024) return launch_fused_t<K, W, 1024>(stream, n_blocks, lds_bytes, A);

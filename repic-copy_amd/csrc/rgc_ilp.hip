@@ -19,6 +19,7 @@
 //      summed in f64 (exact), so "optimal" is exact.  A component that exceeds the node
 //      limit keeps the best packing found and is reported as not proven optimal.
 #include "rgc_kernels.h"
+#include "../../include/repic_gc.h"
 
 #include <climits>
 
@@ -463,6 +464,277 @@ __global__ __launch_bounds__(64) void k_ilp_wave(IlpArgs A, int n_big) {
     }
     wave_sync();
   }
+}
+
+// ----------------------------------------------------------------------------- certification
+// Components the branch and bound did not prove optimal: more than ILP_BIG cliques (never
+// searched) or node_limit hit.  Gurobi (run_ilp.py:50-63, default parameters) reports a model
+// optimal once its bound is within MIPGap = 1e-4 (relative) of the incumbent, so these get:
+//   * a primal packing: the B&B incumbent, or for unsearched components the greedy packing by
+//     (weight desc, column asc) - computed in parallel rounds, a clique joins when it is the
+//     heaviest undecided clique on every one of its boxes (same result as the sequential
+//     greedy) - then improving swaps (add a clique, drop the chosen cliques on its boxes)
+//     claimed per box by gain, rounds until none improves;
+//   * a dual bound: the Lagrangian relaxation of the box constraints, L(lam) = sum_r lam_r +
+//     sum_c max(0, w_c - sum_{r in c} lam_r) >= OPT for every lam >= 0, lowered by projected
+//     subgradient steps (per component, Polyak step towards the primal);
+//   * RGC_ILP_GAP_OK when lbest - primal <= 1e-4 primal, else the packing with status
+//     NODE_LIMIT / HEURISTIC.
+constexpr uint8_t ST_UND = 0, ST_IN = 1, ST_OUT = 2, ST_NONE = 3;
+constexpr int CS = 8;   // doubles per component record: lsum g2 lbest mu primal step stall pad
+
+__device__ __forceinline__ int64_t ilp_comp(const IlpArgs& A, int64_t c) {
+  return A.comp_id[A.parent[c]];
+}
+__device__ __forceinline__ int64_t ilp_row_comp(const IlpArgs& A, int64_t r) {
+  return A.rptr[r + 1] > A.rptr[r] ? ilp_comp(A, A.rcols[A.rptr[r]]) : -1;
+}
+
+// per component: what the branch and bound left unproven
+__global__ __launch_bounds__(ILP_WG) void k_cert_flag(IlpArgs A) {
+  const int64_t comp = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (comp >= A.n_comp) return;
+  const int n = A.comp_n[comp];
+  uint8_t f = 0;
+  if (n > ILP_BIG) f = 2;
+  else if (n > 1 && A.exact[A.members[A.comp_off[comp]]] == 0) f = 1;
+  A.cert[comp] = f;
+  double* cs = A.cs + comp * CS;
+  cs[0] = 0.0; cs[1] = 0.0; cs[2] = INFINITY; cs[3] = 2.0; cs[4] = 0.0; cs[5] = 0.0; cs[6] = 0.0;
+}
+
+// per column: priority key and state; chosen columns of node-limit components own their rows
+__global__ __launch_bounds__(ILP_WG) void k_cert_cols(IlpArgs A) {
+  const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (c >= A.n_cols) return;
+  const uint8_t f = A.cert[ilp_comp(A, c)];
+  const double w = A.w[c];
+  A.key[c] = ((uint64_t)__float_as_uint((float)fmax(w, 0.0)) << 32) | (uint32_t)~(uint32_t)c;
+  uint8_t st = ST_NONE;
+  if (f == 2) st = w > 0.0 ? ST_UND : ST_OUT;
+  else if (f == 1) st = A.x[c] ? ST_IN : ST_OUT;
+  A.st[c] = st;
+  if (st == ST_IN)
+    for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e) A.owner[A.row_idx[e]] = (int32_t)c;
+}
+
+__global__ __launch_bounds__(ILP_WG) void k_cert_rows_init(IlpArgs A) {
+  const int64_t r = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (r >= A.n_rows) return;
+  A.owner[r] = -1;
+  A.rmax[r] = 0;
+  A.grad[r] = 0.0;
+  A.lam[r] = 0.0;
+}
+
+// greedy round: claims, winners, losers (the heaviest undecided clique on each of its boxes
+// joins; cliques on a taken box leave; the rest reset their boxes' claims)
+__global__ __launch_bounds__(ILP_WG) void k_gr_claim(IlpArgs A) {
+  const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (c >= A.n_cols || A.st[c] != ST_UND) return;
+  const unsigned long long k = A.key[c];
+  for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e)
+    atomicMax(reinterpret_cast<unsigned long long*>(A.rmax + A.row_idx[e]), k);
+}
+__global__ __launch_bounds__(ILP_WG) void k_gr_win(IlpArgs A) {
+  const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (c >= A.n_cols || A.st[c] != ST_UND) return;
+  bool win = true;
+  for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e) win &= A.rmax[A.row_idx[e]] == A.key[c];
+  if (!win) return;
+  A.st[c] = ST_IN;
+  for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e) A.owner[A.row_idx[e]] = (int32_t)c;
+}
+__global__ __launch_bounds__(ILP_WG) void k_gr_lose(IlpArgs A) {
+  const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (c >= A.n_cols || A.st[c] != ST_UND) return;
+  bool hit = false;
+  for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e) hit |= A.owner[A.row_idx[e]] >= 0;
+  if (hit) {
+    A.st[c] = ST_OUT;
+    return;
+  }
+  for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e) A.rmax[A.row_idx[e]] = 0;
+  atomicAdd(A.count, 1u);
+}
+
+// swap round: an unchosen clique whose weight exceeds the chosen cliques on its boxes claims
+// its boxes and those cliques' boxes by gain; winners (all claims held) swap in
+__device__ __forceinline__ int swap_victims(const IlpArgs& A, int64_t c, int32_t (&v)[8]) {
+  int nv = 0;
+  for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e) {
+    const int32_t o = A.owner[A.row_idx[e]];
+    if (o < 0) continue;
+    bool seen = false;
+    for (int i = 0; i < nv; ++i) seen |= v[i] == o;
+    if (!seen) v[nv++] = o;
+  }
+  return nv;
+}
+__device__ __forceinline__ bool swap_gain(const IlpArgs& A, int64_t c, uint64_t* key) {
+  int32_t v[8];
+  const int nv = swap_victims(A, c, v);
+  double lost = 0.0;
+  for (int i = 0; i < nv; ++i) lost += A.w[v[i]];
+  const double gain = A.w[c] - lost;
+  if (!(gain > 1e-12 * A.w[c])) return false;
+  *key = ((uint64_t)__float_as_uint((float)gain) << 32) | (uint32_t)~(uint32_t)c;
+  return true;
+}
+template <int STEP>
+__global__ __launch_bounds__(ILP_WG) void k_ls(IlpArgs A) {
+  const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (c >= A.n_cols || A.st[c] != ST_OUT) return;
+  uint64_t key;
+  if (!swap_gain(A, c, &key)) return;
+  int32_t v[8];
+  const int nv = swap_victims(A, c, v);
+  auto each_row = [&](auto&& fn) {
+    for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e) fn(A.row_idx[e]);
+    for (int i = 0; i < nv; ++i)
+      for (int64_t e = A.col_ptr[v[i]]; e < A.col_ptr[v[i] + 1]; ++e) fn(A.row_idx[e]);
+  };
+  if (STEP == 0) {          // claim
+    each_row([&](int32_t r) { atomicMax(reinterpret_cast<unsigned long long*>(A.rmax + r), key); });
+  } else if (STEP == 1) {   // winners: drop the victims (their boxes freed), mark the winner
+    bool win = true;
+    each_row([&](int32_t r) { win &= A.rmax[r] == key; });
+    if (!win) return;
+    for (int i = 0; i < nv; ++i) {
+      A.st[v[i]] = ST_OUT;
+      for (int64_t e = A.col_ptr[v[i]]; e < A.col_ptr[v[i] + 1]; ++e) A.owner[A.row_idx[e]] = -1;
+    }
+    A.st[c] = 4;   // (swapping in: takes its boxes in the next step)
+    atomicAdd(A.count, 1u);
+  }
+}
+__global__ __launch_bounds__(ILP_WG) void k_ls_take(IlpArgs A) {
+  const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (c >= A.n_cols) return;
+  if (A.st[c] == 4) {
+    A.st[c] = ST_IN;
+    for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e) A.owner[A.row_idx[e]] = (int32_t)c;
+  }
+}
+__global__ __launch_bounds__(ILP_WG) void k_ls_clear(IlpArgs A) {
+  const int64_t r = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (r < A.n_rows) A.rmax[r] = 0;
+}
+
+// primal value per component and the initial multipliers lam_r = max_{c on r} w_c / |c|
+// (every reduced cost <= 0: L(lam0) = sum_r lam_r)
+__global__ __launch_bounds__(ILP_WG) void k_lr_init(IlpArgs A) {
+  const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (c >= A.n_cols || A.st[c] == ST_NONE) return;
+  const int64_t comp = ilp_comp(A, c);
+  if (A.st[c] == ST_IN) atomicAdd(A.cs + comp * CS + 4, A.w[c]);
+  const double share = fmax(A.w[c], 0.0) / (double)(A.col_ptr[c + 1] - A.col_ptr[c]);
+  for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e)
+    atomicMax(reinterpret_cast<unsigned long long*>(A.lam + A.row_idx[e]),
+              (unsigned long long)__double_as_longlong(share));   // (non-negative doubles)
+}
+// one subgradient iteration: reduced costs -> cover counts -> L, |g|^2 -> step -> lam
+__global__ __launch_bounds__(ILP_WG) void k_lr_cols(IlpArgs A) {
+  const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (c >= A.n_cols || A.st[c] == ST_NONE) return;
+  double rc = A.w[c];
+  for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e) rc -= A.lam[A.row_idx[e]];
+  if (!(rc > 0.0)) return;
+  atomicAdd(A.cs + ilp_comp(A, c) * CS + 0, rc);
+  for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e) atomicAdd(A.grad + A.row_idx[e], 1.0);
+}
+__global__ __launch_bounds__(ILP_WG) void k_lr_rows(IlpArgs A) {
+  const int64_t r = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (r >= A.n_rows) return;
+  const int64_t comp = ilp_row_comp(A, r);
+  if (comp < 0 || A.cert[comp] == 0) return;
+  double g = 1.0 - A.grad[r];           // d L / d lam_r
+  if (A.lam[r] <= 0.0 && g > 0.0) g = 0.0;   // projected: lam stays at 0
+  A.grad[r] = g;
+  double* cs = A.cs + comp * CS;
+  atomicAdd(cs + 0, A.lam[r]);
+  atomicAdd(cs + 1, g * g);
+}
+__global__ __launch_bounds__(ILP_WG) void k_lr_step(IlpArgs A) {
+  const int64_t comp = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (comp >= A.n_comp || A.cert[comp] == 0) return;
+  double* cs = A.cs + comp * CS;
+  const double L = cs[0], g2 = cs[1], P = cs[4];
+  if (L < cs[2]) {
+    if (L < cs[2] - 1e-9 * fabs(cs[2])) cs[6] = 0.0; else cs[6] += 1.0;
+    cs[2] = L;
+  } else {
+    cs[6] += 1.0;
+  }
+  if (cs[6] >= 8.0) { cs[3] *= 0.5; cs[6] = 0.0; }
+  cs[5] = g2 > 0.0 ? cs[3] * fmax(L - P, 0.0) / g2 : 0.0;
+  cs[0] = 0.0;
+  cs[1] = 0.0;
+}
+__global__ __launch_bounds__(ILP_WG) void k_lr_lam(IlpArgs A) {
+  const int64_t r = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (r >= A.n_rows) return;
+  const int64_t comp = ilp_row_comp(A, r);
+  if (comp < 0 || A.cert[comp] == 0) return;
+  A.lam[r] = fmax(0.0, A.lam[r] - A.cs[comp * CS + 5] * A.grad[r]);
+  A.grad[r] = 0.0;
+}
+// x and the component statuses
+__global__ __launch_bounds__(ILP_WG) void k_cert_final(IlpArgs A) {
+  const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (c >= A.n_cols || A.st[c] == ST_NONE) return;
+  const int64_t comp = ilp_comp(A, c);
+  const double* cs = A.cs + comp * CS;
+  A.x[c] = A.st[c] == ST_IN ? 1 : 0;
+  const double P = cs[4], Lb = cs[2];
+  const bool ok = Lb - P <= 1e-4 * fabs(P);
+  A.exact[c] = ok ? RGC_ILP_GAP_OK : (A.cert[comp] == 2 ? RGC_ILP_HEURISTIC : RGC_ILP_NODE_LIMIT);
+}
+// (before k_lr_init: the primal value is recounted from the final packing)
+__global__ __launch_bounds__(ILP_WG) void k_cert_reset_primal(IlpArgs A) {
+  const int64_t comp = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (comp < A.n_comp) A.cs[comp * CS + 4] = 0.0;
+}
+
+void launch_ilp_cert(hipStream_t stream, int phase, const IlpArgs& A) {
+  const int64_t nbc = (A.n_cols + ILP_WG - 1) / ILP_WG;
+  const int64_t nbr = (A.n_rows + ILP_WG - 1) / ILP_WG;
+  const int64_t nbk = (A.n_comp + ILP_WG - 1) / ILP_WG;
+  if (!nbc) return;
+#define RGC_L(kern, nb) hipLaunchKernelGGL(kern, dim3(nb), dim3(ILP_WG), 0, stream, A)
+  switch (phase) {
+    case 0:
+      RGC_L(k_cert_flag, nbk);
+      if (nbr) RGC_L(k_cert_rows_init, nbr);
+      RGC_L(k_cert_cols, nbc);
+      break;
+    case 1:
+      RGC_L(k_gr_claim, nbc);
+      RGC_L(k_gr_win, nbc);
+      RGC_L(k_gr_lose, nbc);
+      break;
+    case 2:
+      RGC_L((k_ls<0>), nbc);
+      RGC_L((k_ls<1>), nbc);
+      RGC_L(k_ls_take, nbc);
+      if (nbr) RGC_L(k_ls_clear, nbr);
+      break;
+    case 3:
+      RGC_L(k_cert_reset_primal, nbk);
+      if (nbr) RGC_L(k_cert_rows_init, nbr);   // (owner no longer needed)
+      RGC_L(k_lr_init, nbc);
+      break;
+    case 4:
+      RGC_L(k_lr_cols, nbc);
+      if (nbr) RGC_L(k_lr_rows, nbr);
+      RGC_L(k_lr_step, nbk);
+      if (nbr) RGC_L(k_lr_lam, nbr);
+      break;
+    case 5:
+      RGC_L(k_cert_final, nbc);
+      break;
+  }
+#undef RGC_L
 }
 
 int ilp_small_max() { return ILP_SMALL; }

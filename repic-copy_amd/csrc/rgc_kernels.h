@@ -256,10 +256,23 @@ struct IlpArgs {
   uint64_t* wscratch;         // wave solver: wstride words per wave
   int64_t wstride;
   uint8_t* x;                 // [n_cols] solution
-  uint8_t* exact;             // [n_cols] 1 = component proven optimal
+  uint8_t* exact;             // [n_cols] RGC_ILP_* status of the column's component
+  // certification stage (components not proven optimal by the branch and bound)
+  uint8_t* cert;              // [n_comp] 0 proven, 1 node limit, 2 too large to search
+  uint64_t* key;              // [n_cols] greedy / swap priority
+  uint8_t* st;                // [n_cols] 0 undecided, 1 chosen, 2 not chosen, 3 not certified
+  uint64_t* rmax;             // [n_rows] claims
+  int32_t* owner;             // [n_rows] chosen column covering the row, -1
+  double* lam;                // [n_rows] Lagrange multipliers
+  double* grad;               // [n_rows] subgradient (cover count in between)
+  double* cs;                 // [n_comp * 8] per component: lsum g2 lbest mu primal step stall
+  unsigned int* count;        // round counter
 };
 int ilp_small_max();
 int ilp_big_max();
 void launch_ilp(hipStream_t stream, int phase, const IlpArgs& A, int n_big, int n_waves);
+// certification stage (rgc_ilp.hip): phase 0 setup, 1 greedy round, 2 swap round, 3 primal
+// and multiplier init, 4 subgradient iteration, 5 final statuses
+void launch_ilp_cert(hipStream_t stream, int phase, const IlpArgs& A);
 
 }  // namespace rgc

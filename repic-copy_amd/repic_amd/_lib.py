@@ -100,6 +100,12 @@ def abi_version() -> int:
     return lib.rgc_abi_version()
 
 
+def ilp_big_max() -> int:
+    """Largest conflict component (cliques) the run_ilp branch and bound searches
+    (rgc_ilp.hip ILP_BIG); larger ones are certified, not searched."""
+    return 4096
+
+
 # ----------------------------------------------------------------------------- parsing
 def parse_files(paths, n_threads=None):
     """Parse BOX files with the C++ parser -> (status[n], off[n+1], x, y, score, sigmoid)."""
@@ -109,22 +115,38 @@ def parse_files(paths, n_threads=None):
     if n_threads is None:
         n_threads = min(16, os.cpu_count() or 1)
     _check(lib.rgc_parse_files(arr, n, int(n_threads), C.byref(out)))
-    try:
-        P = out.contents
-        status = np.ctypeslib.as_array(P.status, shape=(n,)).copy() if n else np.zeros(0, np.int32)
-        off = np.ctypeslib.as_array(P.off, shape=(n + 1,)).copy()
-        tot = int(off[-1])
-        if tot:
-            x = np.ctypeslib.as_array(P.x, shape=(tot,)).copy()
-            y = np.ctypeslib.as_array(P.y, shape=(tot,)).copy()
-            s = np.ctypeslib.as_array(P.score, shape=(tot,)).copy()
-        else:
-            x = y = s = np.zeros(0, np.float64)
-        sig = (np.ctypeslib.as_array(P.sigmoid, shape=(n,)).astype(bool) if n
-               else np.zeros(0, bool))
-    finally:
-        lib.rgc_parsed_free(out)
+    # the library-owned x / y / score arrays are handed out without a copy: each numpy view's
+    # base is a ctypes array holding the owner, which frees them when the last view is gone
+    owner = _ParsedOwner(out)
+    P = out.contents
+    status = np.ctypeslib.as_array(P.status, shape=(n,)).copy() if n else np.zeros(0, np.int32)
+    off = np.ctypeslib.as_array(P.off, shape=(n + 1,)).copy()
+    tot = int(off[-1])
+    if tot:
+        x, y, s = (owner.view(p, tot) for p in (P.x, P.y, P.score))
+    else:
+        x = y = s = np.zeros(0, np.float64)
+    sig = (np.ctypeslib.as_array(P.sigmoid, shape=(n,)).astype(bool) if n
+           else np.zeros(0, bool))
     return status, off, x, y, s, sig
+
+
+class _ParsedOwner:
+    """Frees an rgc_parsed once no numpy view of its arrays is left."""
+
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    def view(self, p, n):
+        ca = (C.c_double * n).from_address(C.cast(p, C.c_void_p).value)
+        ca._owner = self
+        return np.frombuffer(ca, dtype=np.float64)
+
+    def __del__(self):
+        try:
+            lib.rgc_parsed_free(self.ptr)
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
 
 
 # ----------------------------------------------------------------------------- CPython set order

@@ -23,8 +23,8 @@ import numpy as np
 
 from .. import _lib
 from ..dist import agree, pair_work, reduce_counts, shard_bounds
-from ..ingest import DirIndex, list_methods, micrograph_names, plan, probe_start_method
-from ..pipeline import Batch, run_batch, split_batches
+from ..ingest import DirIndex, list_methods, micrograph_names, plan_chunk, probe_start_method
+from ..pipeline import split_batches
 from ..writers import Writer, multi_out_coords
 
 name = "get_cliques"
@@ -121,7 +121,7 @@ def _main(args, ctx, world, rank):
     if world > 1:
         import torch.distributed as dist
         if not dist.is_initialized():
-            dist.init_process_group("gloo")   # control-plane only: a few int64 per rank
+            dist.init_process_group(_dist_backend(world))
     assert os.path.exists(args.in_dir), "Error - input directory does not exist"
     # checked before anything is deleted: the device kernels are compiled for k <= MAX_K
     k_pre = len(_methods_after_reset(args.in_dir, args.out_dir))
@@ -142,123 +142,334 @@ def _main(args, ctx, world, rank):
     names = micrograph_names(index, methods)
     t_index = time.time() - t_start
     lo, hi = 0, len(names)
-    # large runs write from spawned processes, started now so they import during the parse
-    # and the device work
-    writer = Writer(getattr(args, "threads", None),
-                    processes=len(names) >= PROC_WRITER_MIN * max(1, world))
     if dist is not None:
         b = shard_bounds(_shard_weights(args.in_dir, methods, index, names), world)
         lo, hi = b[rank], b[rank + 1]
-    k = len(methods)
-    t_plan = time.time()
-    mgs, results, err, consumed = [], {}, None, 0
+    run = _Run(args, ctx, methods, index, names[lo:hi], lo)
+    writer = None
     try:
-        mgs, crash, consumed = plan(args.in_dir, methods, index, order=names[lo:hi],
-                                    n_threads=getattr(args, "threads", None))
-    except Exception as e:  # noqa: BLE001 - re-raised by agree() after the exchange
-        err = e
-    if dist is not None:
-        # global box-id offset of this shard (the one data exchange), with failure agreement
-        cons = agree(err, [consumed])
-        id_off = sum(c[0] for c in cons[:rank])
-        for mg in mgs:
-            mg.id_base += id_off
-    elif err is not None:
-        raise err
-    ok = [mg for mg in mgs if mg.status == "ok"]
-    t_plan = time.time() - t_plan
-    t_dev = 0.0
-    n_edges = n_cliques = 0
-    try:
-        if ok:
-            counts = [sum(c.n for c in mg.coords) for mg in ok]
-            for m0, m1 in split_batches(counts, getattr(args, "batch_boxes", 1 << 25)):
-                part = ok[m0:m1]
-                batch = Batch.pack(k, args.box_size, [[(c.x, c.y, c.s) for c in mg.coords]
-                                                     for mg in part],
-                                   id_bases=[mg.id_base for mg in part])
-                t0 = time.time()
-                res = run_batch(ctx, batch, get_cc=args.get_cc, multi_out=args.multi_out)
-                t_dev += time.time() - t0
-                for j, mg in enumerate(part):
-                    results[id(mg)] = (batch, j, res[j])
-                    n_edges += res[j].n_edges
-                    n_cliques += len(res[j].w)
-    except Exception as e:  # noqa: BLE001
+        # large runs write from spawned processes, started now so they import during the
+        # parse and the device work
+        writer = Writer(getattr(args, "threads", None),
+                        processes=len(names) >= PROC_WRITER_MIN * max(1, world))
         if dist is None:
-            raise
-        err = e
-    # first micrograph (global index) at which the reference would raise
-    fail = None
-    if err is None:
-        for i, mg in enumerate(mgs):
-            if mg.status == "crash" or (mg.status == "ok" and
-                                        results[id(mg)][2].status != _lib.OK):
-                fail = lo + i
-                break
-    if dist is not None:
-        big = np.iinfo(np.int64).max
-        rows = agree(err, [big if fail is None else fail])
-        gfail = min(r[0] for r in rows)
-        gfail = None if gfail == big else gfail
-    else:
-        gfail = fail
-    share = (t_plan + t_dev) / max(1, len(mgs))
-    t_write = time.time()
-    try:
-        _write_all(args, mgs, results, methods, k, lo, fail, gfail, share, writer)
+            run.stream(writer)
+        else:
+            run.sharded(writer, dist, rank)
     finally:
-        writer.close()
+        t_w = time.time()
+        if writer is not None:
+            writer.close()
+        run.stats["write_tail_s"] = time.time() - t_w
         LAST_RUN.clear()
-        LAST_RUN.update(index_s=t_index, parse_s=t_plan, device_s=t_dev,
-                        write_s=time.time() - t_write, total_s=time.time() - t_start,
-                        micrographs=len(ok), edges=n_edges, cliques=n_cliques)
-        if dist is not None:
-            # node-level counters: one reduction at the end of the run
-            tot = reduce_counts([len(ok), n_edges, n_cliques])
+        LAST_RUN.update(index_s=t_index, total_s=time.time() - t_start, **run.stats)
+        if dist is not None and run.stats.get("reduce", True):
+            # node-level counters: one reduction at the end of the run, over
+            # RCCL when every rank owns its own GPU
+            st = run.stats
+            tot = reduce_counts([st["micrographs"], st["edges"], st["cliques"]],
+                                device=_counter_device(ctx))
             if rank == 0:
                 print(f"get_cliques: {tot[0]} micrographs, {tot[1]} edges, {tot[2]} cliques "
                       f"on {world} ranks")
     sys.stdout.flush()
 
 
-def _write_all(args, mgs, results, methods, k, lo, fail, gfail, share, writer):
-    """Write outputs in reference order; raise the reference's exception where it would."""
-    for i, mg in enumerate(mgs):
-        if gfail is not None and lo + i > gfail:
-            break
-        if gfail is not None and lo + i == gfail and fail != gfail:
-            break
-        print(f"\n--- {mg.base} ---\n")
-        if mg.status == "skip":
-            print("Skipping micrograph - not all methods have picked particles...")
-            writer.skip(args.out_dir, mg.base)
-            continue
+def _distinct_gpus(world):
+    """True when every rank of this node can own its own GPU (LOCAL_RANK < device count and
+    the node's ranks fit the devices), so collectives can run over RCCL."""
+    try:
+        lw = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        return 0 < lw <= _lib.device_count() and os.environ.get("RGC_CLI_GLOO") is None
+    except Exception:  # noqa: BLE001
+        return False
+
+
+def _dist_backend(world):
+    """Control-plane collectives (a few int64 per rank) on gloo; with one GPU per rank the
+    device tensors of the end-of-run counter reduction go over RCCL."""
+    return "cpu:gloo,cuda:nccl" if _distinct_gpus(world) else "gloo"
+
+
+def _counter_device(ctx):
+    import torch
+    import torch.distributed as dist
+    if "nccl" in str(dist.get_backend()).lower():
+        torch.cuda.set_device(ctx.device)
+        return torch.device("cuda", ctx.device)
+    return None
+
+
+# micrographs per pipeline chunk (parse of chunk i+1 | device chunk i | writes of chunk i-1)
+CHUNK_MG = 1024
+# micrographs per writer task
+GROUP_MG = 64
+
+
+class _Run:
+    """One rank's pass over its micrographs, chunk by chunk (reference get_cliques.py:108-229
+    order and failure semantics)."""
+
+    def __init__(self, args, ctx, methods, index, names, lo):
+        self.args, self.ctx, self.methods, self.index = args, ctx, methods, index
+        self.names, self.lo = names, lo
+        self.k = len(methods)
+        self.stats = dict(parse_s=0.0, device_s=0.0, write_s=0.0, micrographs=0, edges=0,
+                          cliques=0, chunks=0)
+        self.chunk = max(1, int(getattr(args, "chunk_mg", None) or CHUNK_MG))
+
+    # -- stages
+    def plan_chunks(self):
+        """Planned chunks in order (the id counter runs across them); stops after a crash."""
+        nid = 0
+        for c0 in range(0, len(self.names), self.chunk):
+            t0 = time.time()
+            ch = plan_chunk(self.args.in_dir, self.methods, self.index,
+                            self.names[c0:c0 + self.chunk], self.k, self.args.box_size, nid,
+                            getattr(self.args, "threads", None))
+            ch.first = self.lo + c0
+            ch.parse_s = time.time() - t0
+            nid = ch.consumed
+            yield ch
+            if ch.crash is not None:
+                return
+
+    def device(self, ch):
+        """Device results of a chunk's ok micrographs (flat host copies)."""
+        ch.res = None
+        if ch.batch is None:
+            return
+        t0 = time.time()
+        b = ch.batch
+        for m0, m1 in split_batches(np.diff(b.box_off[::self.k]).tolist(),
+                                    getattr(self.args, "batch_boxes", 1 << 25)):
+            part = b if (m0 == 0 and m1 == b.n_mg) else b.slice(m0, m1)
+            r = _FlatResult(self.ctx, part, self.args.get_cc, self.args.multi_out,
+                            getattr(self.args, "no_fused", False))
+            ch.res = r if ch.res is None else ch.res.append(r, int(b.box_off[m0 * self.k]))
+        self.stats["device_s"] += time.time() - t0
+        ok = ch.res.status == _lib.OK
+        self.stats["edges"] += int(ch.res.n_edges_mg[ok].sum())
+        self.stats["cliques"] += int(ch.res.clique_cnt[ok].sum())
+
+    def first_failure(self, ch):
+        """Index in ch.mgs of the first micrograph at which the reference raises, or None."""
+        for i, mg in enumerate(ch.mgs):
+            if mg.status == "crash" or (mg.status == "ok" and
+                                        ch.res.status[mg.slot] != _lib.OK):
+                return i
+        return None
+
+    def write(self, ch, writer, stop=None):
+        """Print and write the chunk's micrographs in order up to ``stop`` (exclusive), in
+        groups; returns the micrograph the reference would raise at (if it is < stop)."""
+        mgs = ch.mgs if stop is None else ch.mgs[:stop]
+        share = (ch.parse_s + getattr(ch, "dev_s", 0.0)) / max(1, len(ch.mgs))
+        t0 = time.time()
+        items, slots = [], []
+        raise_at = None
+        for i, mg in enumerate(mgs):
+            print(f"\n--- {mg.base} ---\n")
+            if mg.status == "skip":
+                print("Skipping micrograph - not all methods have picked particles...")
+                items.append((mg.base, -1, 0, 0, 0, 0.0, None))
+                slots.append(-1)
+            elif mg.status == "crash" or ch.res.status[mg.slot] != _lib.OK:
+                raise_at = mg
+                break
+            else:
+                items.append((mg.base, 0, 0, 0, 0, share, None))
+                slots.append(mg.slot)
+                self.stats["micrographs"] += 1
+            if len(items) >= GROUP_MG:
+                self._submit_group(ch, items, slots, writer)
+                items, slots = [], []
+        if items:
+            self._submit_group(ch, items, slots, writer)
+        self.stats["write_s"] += time.time() - t0
+        return raise_at
+
+    @staticmethod
+    def raise_for(mg, ch):
         if mg.status == "crash":
             raise mg.exc
-        t0 = time.time()
-        batch, j, r = results[id(mg)]
-        if r.status == _lib.NO_EDGES:
+        st = ch.res.status[mg.slot]
+        if st == _lib.NO_EDGES:
             raise ValueError("zero-size array to reduction operation maximum which has no identity")
-        if r.status == _lib.NO_CLIQUES:
-            raise UnboundLocalError("local variable 'clique' referenced before assignment")
-        b0 = int(batch.box_off[j * k])
-        idb = int(batch.id_base[j]) - b0
-        cx = cy = cid = coords = None
-        if args.multi_out:
-            def tup(g):
-                return (float(batch.x[g]), float(batch.y[g]), idb + int(g))
-            member_tuples = [[tup(g) for g in row] for row in r.members.tolist()]
-            picker_coords = []
-            for p, c in enumerate(mg.coords):
-                ids = range(idb + int(batch.box_off[j * k + p]),
-                            idb + int(batch.box_off[j * k + p + 1]))
-                ws = list(c.s) if c.sigmoid else c.s.tolist()
-                picker_coords.append(list(zip(c.x.tolist(), c.y.tolist(), ws, ids)))
-            coords = multi_out_coords(methods, member_tuples, r.order.tolist(), k, args.get_cc,
-                                      picker_coords)
+        raise UnboundLocalError("local variable 'clique' referenced before assignment")
+
+    def _submit_group(self, ch, items, slots, writer):
+        r, b, k = ch.res, ch.batch, self.k
+        sl = np.array([s for s in slots if s >= 0], np.int64)
+        if len(sl):
+            cnt = r.clique_cnt[sl]
+            base = r.clique_base[sl]
+            tot = int(cnt.sum())
+            idx = np.repeat(base - (np.cumsum(cnt) - cnt), cnt) + np.arange(tot)
+            g = r.consensus[idx].astype(np.int64)
+            idb = b.id_base[sl] - b.box_off[sl * k]
+            w, conf, rows = r.w[idx], r.conf[idx], r.rows[idx]
+            cx, cy, cid = b.x[g], b.y[g], g + np.repeat(idb, cnt)
         else:
-            g = r.consensus.astype(np.int64)
-            cx, cy, cid = batch.x[g], batch.y[g], idb + g
-        writer.micrograph(args.out_dir, mg.base, r.w, r.conf, r.rows, r.n_vert, cx, cy, cid,
-                          coords, share + (time.time() - t0), r.cc_max, r.cc_cnt)
+            cnt = np.zeros(0, np.int64)
+            w = conf = cx = cy = np.zeros(0)
+            rows = np.zeros((0, k), np.int32)
+            cid = np.zeros(0, np.int64)
+        out, j = [], 0
+        for it, s in zip(items, slots):
+            if s < 0:
+                out.append(it)
+                continue
+            coords = self._multi_out_coords(ch, s) if self.args.multi_out else None
+            out.append((it[0], int(cnt[j]), int(r.n_vert[s]), int(r.cc_max[s]), int(r.cc_cnt[s]),
+                        it[5], coords))
+            j += 1
+        writer.group(self.args.out_dir, out, w, conf, rows, cx, cy, cid)
+
+    def _multi_out_coords(self, ch, s):
+        """--multi_out table of ok micrograph slot s (get_cliques.py:175-178, 206-213)."""
+        r, b, k = ch.res, ch.batch, self.k
+        c0, c1 = int(r.clique_base[s]), int(r.clique_base[s] + r.clique_cnt[s])
+        idb = int(b.id_base[s]) - int(b.box_off[s * k])
+
+        def tup(g):
+            return (float(b.x[g]), float(b.y[g]), idb + int(g))
+        member_tuples = [[tup(g) for g in row] for row in r.members[c0:c1].tolist()]
+        picker_coords = []
+        for p in range(k):
+            p0, p1 = int(b.box_off[s * k + p]), int(b.box_off[s * k + p + 1])
+            sc = b.score[p0:p1]
+            ws = list(sc) if ch.sig[s, p] else sc.tolist()
+            picker_coords.append(list(zip(b.x[p0:p1].tolist(), b.y[p0:p1].tolist(), ws,
+                                          range(idb + p0, idb + p1))))
+        return multi_out_coords(self.methods, member_tuples, r.order[c0:c1].tolist(), k,
+                                self.args.get_cc, picker_coords)
+
+    # -- drivers
+    def stream(self, writer):
+        """Single rank: a parser thread plans chunk i+1 (the C++ parse releases the GIL) while
+        this thread runs chunk i on the device and hands its writes to the writer pool."""
+        import queue
+        import threading
+        q = queue.Queue(maxsize=2)
+        stop = threading.Event()
+
+        def produce():
+            try:
+                for ch in self.plan_chunks():
+                    while not stop.is_set():
+                        try:
+                            q.put(ch, timeout=0.1)
+                            break
+                        except queue.Full:
+                            continue
+                    if stop.is_set():
+                        return
+            except BaseException as e:  # noqa: BLE001 - re-raised by the consumer
+                q.put(e)
+                return
+            q.put(None)
+
+        th = threading.Thread(target=produce, name="rgc-parse", daemon=True)
+        th.start()
+        try:
+            while True:
+                ch = q.get()
+                if ch is None:
+                    break
+                if isinstance(ch, BaseException):
+                    raise ch
+                self.stats["parse_s"] += ch.parse_s
+                self.stats["chunks"] += 1
+                t0 = time.time()
+                self.device(ch)
+                ch.dev_s = time.time() - t0
+                bad = self.write(ch, writer)
+                if bad is not None:
+                    writer.close()        # every earlier micrograph's files exist first
+                    self.raise_for(bad, ch)
+        finally:
+            stop.set()
+            th.join()
+
+    def sharded(self, writer, dist, rank):
+        """One shard of a multi-rank run: plan every chunk (the shard's id offset needs all
+        lower shards' consumed ids), run the device, agree on the first failing micrograph,
+        then write up to it (no rank writes past a micrograph at which the reference raises)."""
+        chunks, err = [], None
+        try:
+            for ch in self.plan_chunks():
+                self.stats["parse_s"] += ch.parse_s
+                chunks.append(ch)
+        except Exception as e:  # noqa: BLE001 - re-raised by agree() after the exchange
+            err = e
+        consumed = chunks[-1].consumed if chunks else 0
+        cons = agree(err, [consumed])
+        id_off = sum(c[0] for c in cons[:rank])
+        fail = None
+        try:
+            for ch in chunks:
+                ch.shift_ids(id_off)
+                t0 = time.time()
+                self.device(ch)
+                ch.dev_s = time.time() - t0
+                self.stats["chunks"] += 1
+                i = self.first_failure(ch)
+                if i is not None and fail is None:
+                    fail = ch.first + i
+        except Exception as e:  # noqa: BLE001
+            err = e
+        big = np.iinfo(np.int64).max
+        rows = agree(err, [big if fail is None else fail])
+        gfail = min(r_[0] for r_ in rows)
+        for ch in chunks:
+            if gfail != big and gfail < ch.first:
+                break                      # a lower rank's micrograph raises first
+            stop = None
+            if gfail != big and gfail < ch.first + len(ch.mgs):
+                stop = gfail - ch.first
+            self.write(ch, writer, stop)
+            if stop is not None:
+                if fail == gfail:          # this rank's own micrograph: earlier files, then raise
+                    writer.close()
+                    self.raise_for(ch.mgs[stop], ch)
+                break
+
+
+class _FlatResult:
+    """Host copies of one device run's outputs (the library's buffers are reused by the next
+    run, which may start before these are written)."""
+
+    PER_MG = ("status", "cc_max", "cc_cnt", "n_vert", "n_edges_mg", "clique_base", "clique_cnt")
+
+    def __init__(self, ctx, batch, get_cc, multi_out, no_fused=False):
+        flags = _lib.F_HOST_OUTPUTS
+        if no_fused:
+            flags |= _lib.F_NO_FUSED
+        if get_cc:
+            flags |= _lib.F_GET_CC
+        if multi_out:
+            flags |= _lib.F_MULTI_OUT
+        r = ctx.run(batch.n_mg, batch.k, batch.box_size, batch.box_off, batch.id_base, batch.x,
+                    batch.y, batch.score, flags)
+        for f in self.PER_MG:
+            setattr(self, f, np.array(getattr(r, f)))
+        self.rows, self.w, self.conf = r.rows.copy(), r.w.copy(), r.conf.copy()
+        self.consensus = r.consensus.copy()
+        self.members = r.members.copy() if r.members is not None else None
+        self.order = r.order.copy() if r.order is not None else None
+
+    def append(self, o, box0):
+        """Concatenate a later sub-batch's result (its box indices start at box0)."""
+        C = len(self.w)
+        for f in self.PER_MG:
+            setattr(self, f, np.concatenate([getattr(self, f), getattr(o, f)]))
+        self.clique_base[-len(o.status):] += C
+        self.rows = np.concatenate([self.rows, o.rows])
+        self.w = np.concatenate([self.w, o.w])
+        self.conf = np.concatenate([self.conf, o.conf])
+        self.consensus = np.concatenate([self.consensus, o.consensus + box0])
+        if self.members is not None:
+            self.members = np.concatenate([self.members, o.members + box0])
+            self.order = np.concatenate([self.order, o.order]) if self.order is not None else None
+        return self

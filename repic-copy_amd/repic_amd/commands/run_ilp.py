@@ -8,12 +8,15 @@ directory in one device batch (repic_amd.ilp), then writes what the reference wr
 order: ``<base>.box`` (chosen cliques' consensus coordinates by decreasing confidence, rounded
 with np.rint, :112-124) and one more line of ``<base>_runtime.tsv`` (:127-131).
 
-Differences, stated: Gurobi stops at a 1e-4 relative MIP gap by default; this solver is exact
-(f32 weights summed in f64), and picks, among equally good packings, the one its
-heaviest-first branch order meets first (Gurobi's choice among ties is unspecified).  Lines
+Differences, stated: Gurobi stops at a 1e-4 relative MIP gap by default; this solver proves
+conflict components of up to 4096 cliques optimal exactly (f32 weights summed in f64) and
+picks, among equally good packings, the one its heaviest-first branch order meets first
+(Gurobi's choice among ties is unspecified).  Larger components, and components that exceed
+``--node_limit``, get a greedy + swap local-search packing (or the branch and bound's best)
+certified by a Lagrangian dual bound: within Gurobi's default 1e-4 gap it is accepted silently,
+as Gurobi would; otherwise a warning names the micrograph and says which case it is.  Lines
 of equal confidence follow our clique column order (the reference's is CPython set order,
-not reproducible, get_cliques.py:161).  A component that exceeds ``--node_limit`` keeps the
-best packing found and a warning names the micrograph.  With ``--multi_out`` inputs the
+not reproducible, get_cliques.py:161).  With ``--multi_out`` inputs the
 reference raises AttributeError (``confidences`` is a tuple there, :97-106); so does this.
 """
 from __future__ import annotations
@@ -26,7 +29,7 @@ import time
 
 import numpy as np
 
-from .. import _lib
+from .. import _lib, ilp
 from ..ilp import solve_batch
 
 name = "run_ilp"
@@ -70,11 +73,12 @@ def main(args):
             break
         mats.append(A)
         weights.append(w)
-    xs, exact = [], []
+    xs, status = [], []
     if mats:
         ctx = _lib.Context(dev)
         try:
-            xs, exact = solve_batch(ctx, mats, weights, getattr(args, "node_limit", 0))
+            xs, status = solve_batch(ctx, mats, weights, getattr(args, "node_limit", 0),
+                                     statuses=True)
         finally:
             ctx.close()
     share = (time.time() - t0) / max(1, len(mats))
@@ -85,9 +89,15 @@ def main(args):
         if i == len(mats):
             raise err
         A, x = mats[i], xs[i].astype(np.float64)
-        if not exact[i]:
-            print(f"Warning - {base}: node limit reached in a conflict component, the packing "
-                  f"is the best found (not proven optimal)", file=sys.stderr)
+        if status[i] == ilp.NODE_LIMIT:
+            print(f"Warning - {base}: node limit reached in a conflict component and its "
+                  f"Lagrangian bound leaves a gap above 1e-4: the packing is the best found, "
+                  f"not proven optimal", file=sys.stderr)
+        elif status[i] == ilp.HEURISTIC:
+            print(f"Warning - {base}: a conflict component of more than "
+                  f"{_lib.ilp_big_max()} cliques was not searched; the packing is greedy + "
+                  f"swap local search and its Lagrangian bound leaves a gap above 1e-4",
+                  file=sys.stderr)
         # run_ilp.py:66-69: every vertex at most once, and at least one clique chosen
         assert np.max(A.tocsr() @ x) == 1, "Error - vertices are assigned to multiple cliques"
         coords = _load(mf.replace("_constraint_matrix", "_consensus_coords"))

@@ -40,9 +40,25 @@ def pack(mats):
     return col_ptr, row_idx, row0, np.asarray(col_off, np.int64)
 
 
-def solve_batch(ctx, mats, weights, node_limit=0, timing=False):
+# component statuses (include/repic_gc.h RGC_ILP_*)
+NODE_LIMIT, OPTIMAL, GAP_OK, HEURISTIC = 0, 1, 2, 3
+
+
+def mg_status(ex):
+    """A micrograph's status from its columns' component statuses: the weakest one
+    (HEURISTIC < NODE_LIMIT < GAP_OK < OPTIMAL)."""
+    if len(ex) == 0:
+        return OPTIMAL
+    for st in (HEURISTIC, NODE_LIMIT, GAP_OK):
+        if (ex == st).any():
+            return st
+    return OPTIMAL
+
+
+def solve_batch(ctx, mats, weights, node_limit=0, timing=False, statuses=False):
     """Returns (x list of uint8 arrays, exact list of bool): per micrograph the chosen
-    columns and whether every component was proven optimal."""
+    columns and whether every component was proven optimal (with ``statuses``: the
+    micrograph status codes, mg_status, instead of the bools)."""
     col_ptr, row_idx, n_rows, col_off = pack(mats)
     w = np.ascontiguousarray(np.concatenate([np.asarray(v, np.float64).ravel() for v in weights])
                              if weights else np.zeros(0), dtype=np.float64)
@@ -56,5 +72,7 @@ def solve_batch(ctx, mats, weights, node_limit=0, timing=False):
                int(node_limit), _lib.F_TIMING if timing else 0)
     _lib._check(_lib.lib.rgc_ilp_solve(ctx._p, C.byref(si), x.ctypes.data, ex.ctypes.data))
     xs = [x[col_off[m]:col_off[m + 1]] for m in range(len(mats))]
-    exact = [bool(ex[col_off[m]:col_off[m + 1]].all()) for m in range(len(mats))]
-    return xs, exact
+    st = [mg_status(ex[col_off[m]:col_off[m + 1]]) for m in range(len(mats))]
+    if statuses:
+        return xs, st
+    return xs, [s_ == OPTIMAL for s_ in st]

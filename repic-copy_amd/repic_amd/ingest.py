@@ -194,7 +194,8 @@ class Micrograph:
     status: str = "ok"             # ok | skip | crash
     exc: BaseException | None = None
     id_base: int = 0
-    coords: list = field(default_factory=list)  # k ParsedFile (ok micrographs)
+    coords: list = field(default_factory=list)  # k ParsedFile (ok micrographs; plan())
+    slot: int = -1                 # index among the chunk's ok micrographs (plan_chunk())
 
 
 def _glob_path_itself(path: str):
@@ -270,3 +271,175 @@ def plan(in_dir, methods, index: DirIndex, order=None, n_threads=None):
     if crash is not None:
         mgs = mgs[:crash + 1]
     return mgs, crash, next_id
+
+
+# ----------------------------------------------------------------------------- chunked plan
+class Chunk:
+    """One chunk of the reference-order micrograph list, planned and parsed.
+
+    ``mgs``: Micrograph records (status ok / skip / crash; ok ones carry ``id_base`` and
+    ``slot``, their index in ``batch``).  ``batch``: the packed ok micrographs
+    (pipeline.Batch; None when there is none).  ``sig``: per (ok micrograph, picker) sigmoid
+    flag (the --multi_out table keeps numpy scalars for mapped scores).  ``consumed``: box ids
+    consumed (skips included).  ``crash``: index in ``mgs`` of the micrograph at which the
+    reference raises (its exception in ``exc``; the chunk ends there), else None.
+    """
+
+    def __init__(self, mgs, batch, sig, consumed, crash):
+        self.mgs, self.batch, self.sig, self.consumed, self.crash = mgs, batch, sig, consumed, crash
+
+    def shift_ids(self, off):
+        """Add a global id offset (a shard's exclusive prefix) to every id of the chunk."""
+        for mg in self.mgs:
+            mg.id_base += off
+        if self.batch is not None:
+            self.batch.id_base = self.batch.id_base + off
+
+
+def resolve(in_dir, methods, index: DirIndex, names):
+    """Micrograph records with their k lists of matching paths (get_cliques.py:108-122)."""
+    mgs = []
+    d0 = os.path.join(in_dir, methods[0])
+    others = [(m, os.path.join(in_dir, m)) for m in methods[1:]]
+    for name in names:
+        base = name.replace(".box", "")
+        files = [_glob_path_itself(os.path.join(d0, name))]
+        for m, dm in others:
+            files.append([os.path.join(dm, n) for n in index.glob(m, f"*{base}*")])
+        mgs.append(Micrograph(base=base, files=files))
+    return mgs
+
+
+def plan_chunk(in_dir, methods, index: DirIndex, names, k, box_size, next_id=0,
+               n_threads=None):
+    """Resolve, parse (C++ parser, GIL released) and pack one chunk of micrographs, giving
+    box ids from ``next_id`` on (the process-wide counter of common.py:23,108-112).
+
+    Fast path (the common case: every micrograph has exactly one file per picker, all files
+    distinct and parsed OK): the parser's flat arrays are already the batch layout
+    (micrograph-major, picker order, file order), so ids and offsets are two cumsums.  Any
+    other chunk takes the per-micrograph loop of :func:`plan`'s semantics."""
+    from .pipeline import Batch
+    mgs = resolve(in_dir, methods, index, names)
+    uniq = {}
+    single = True
+    for mg in mgs:
+        for fl in mg.files:
+            if len(fl) != 1:
+                single = False
+            for p in fl:
+                uniq.setdefault(p, len(uniq))
+    paths = list(uniq)
+    if not paths:
+        st = np.zeros(0, np.int32)
+        off = np.zeros(1, np.int64)
+        x = y = sc = np.zeros(0)
+        sg = np.zeros(0, bool)
+    else:
+        st, off, x, y, sc, sg = _lib.parse_files(paths, n_threads)
+        if bool((st == _lib.PARSE_FALLBACK).any()):
+            st, off, x, y, sc, sg = _splice_fallback(paths, st, off, x, y, sc, sg)
+    nf = len(paths)
+    if (single and mgs and nf == len(mgs) * k and
+            bool((st == _lib.PARSE_OK).all())):
+        cnt = np.diff(off)
+        if bool((cnt > 0).all()):
+            per_mg = cnt.reshape(-1, k).sum(axis=1)
+            id_base = next_id + np.concatenate([[0], np.cumsum(per_mg)[:-1]])
+            if sg.any():
+                sc = sc.copy()
+                m = np.repeat(sg, cnt)
+                sc[m] = sigmoid(sc[m])
+            for i, mg in enumerate(mgs):
+                mg.id_base = int(id_base[i])
+                mg.slot = i
+            batch = Batch(k, box_size, off, id_base, x, y, sc)
+            return Chunk(mgs, batch, sg.reshape(-1, k), next_id + int(per_mg.sum()), None)
+    # general path: per micrograph, in order (skips consume ids; the first crash ends it)
+    crash = None
+    ok_files = []
+    for i, mg in enumerate(mgs):
+        mg.id_base = next_id
+        fidx = []
+        try:
+            for fl in mg.files:
+                if not fl:
+                    raise UnboundLocalError("local variable 'i' referenced before assignment")
+                f = None
+                for pth in fl:
+                    f = uniq[pth]
+                    if st[f] != _lib.PARSE_OK:
+                        raise _parsed_exc(int(st[f]), pth)
+                if len(fl) > 1:
+                    raise AssertionError("Error - multiple BOX files found using pattern")
+                fidx.append(f)
+                next_id += int(off[f + 1] - off[f])
+        except (UnboundLocalError, IndexError):
+            mg.status = "skip"
+            continue
+        except BaseException as e:  # noqa: BLE001 - reproduced exception is the contract
+            mg.status, mg.exc = "crash", e
+            crash = i
+            break
+        mg.slot = len(ok_files)
+        ok_files.append(fidx)
+    if crash is not None:
+        mgs = mgs[:crash + 1]
+    if not ok_files:
+        return Chunk(mgs, None, np.zeros((0, k), bool), next_id, crash)
+    fl = np.array(ok_files, np.int64).reshape(-1)
+    cnt = off[fl + 1] - off[fl]
+    box_off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+    src = np.repeat(off[fl] - box_off[:-1], cnt) + np.arange(int(box_off[-1]))
+    bsig = sg[fl]
+    sc2 = sc[src]
+    if bsig.any():
+        m = np.repeat(bsig, cnt)
+        sc2[m] = sigmoid(sc2[m])
+    ok = [mg for mg in mgs if mg.status == "ok"]
+    batch = Batch(k, box_size, box_off, np.array([mg.id_base for mg in ok], np.int64),
+                  x[src], y[src], sc2)
+    return Chunk(mgs, batch, bsig.reshape(-1, k), next_id, crash)
+
+
+def _splice_fallback(paths, st, off, x, y, sc, sg):
+    """Files the C++ parser handed back (non-ASCII bytes) parsed with Python's own str/float
+    semantics and spliced into the flat arrays (status OK, or the status of the exception
+    class they raise; rare, so rebuilt with concatenations)."""
+    st = st.copy()
+    sg = sg.copy()
+    parts = []
+    for f, pth in enumerate(paths):
+        seg = (x[off[f]:off[f + 1]], y[off[f]:off[f + 1]], sc[off[f]:off[f + 1]])
+        if st[f] == _lib.PARSE_FALLBACK:
+            try:
+                xs, ys, ss, sgf = _py_parse(pth)
+                seg = (xs, ys, ss)
+                st[f], sg[f] = _lib.PARSE_OK, sgf
+            except Exception as e:  # noqa: BLE001
+                # skip-class exceptions by status; any other re-raised by _parsed_exc's re-parse
+                st[f] = {IndexError: _lib.PARSE_INDEX}.get(type(e), _lib.PARSE_FALLBACK)
+                seg = (np.zeros(0), np.zeros(0), np.zeros(0))
+        parts.append(seg)
+    cnt = np.array([len(p[0]) for p in parts], np.int64)
+    off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+    cat = lambda j: np.concatenate([p[j] for p in parts]) if parts else np.zeros(0)  # noqa: E731
+    return st, off, cat(0), cat(1), cat(2), sg
+
+
+def _parsed_exc(st, path):
+    """The exception the reference raises for a file the C++ parser flagged (or, for
+    FALLBACK / OSERROR files, Python's own parse of it)."""
+    if st == _lib.PARSE_FALLBACK:
+        try:
+            _py_parse(path)
+        except Exception as e:  # noqa: BLE001
+            return e
+        return None
+    if st == _lib.PARSE_OSERROR:
+        try:
+            open(path, "rt").close()
+            return OSError(f"cannot read {path}")
+        except OSError as e:
+            return e
+    return _EXC[st](path)

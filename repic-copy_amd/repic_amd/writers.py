@@ -83,9 +83,31 @@ def _write_chunk(items):
     for kind, args in items:
         if kind == 0:
             write_skip(*args)
-        else:
+        elif kind == 1:
             write_micrograph_raw(*args)
+        else:
+            write_group(*args)
     return len(items)
+
+
+def write_group(out_dir, items, w, conf, rows, cx, cy, cid):
+    """Writer task for a group of micrographs in reference order, from flat arrays over the
+    group's cliques (micrograph by micrograph): ``items`` = (base, n_cliques, n_vert, cc_max,
+    cc_cnt, seconds, coords) per micrograph, or (base, -1, ...) for a skipped one (empty
+    ``<base>.box``); ``coords`` is the prebuilt --multi_out table, else None and the
+    consensus tuples come from cx / cy / cid."""
+    c0 = 0
+    for base, n, n_vert, cc_max, cc_cnt, seconds, coords in items:
+        if n < 0:
+            write_skip(out_dir, base)
+            continue
+        c1 = c0 + n
+        write_micrograph_raw(out_dir, base, w[c0:c1], conf[c0:c1], rows[c0:c1], n_vert,
+                             cx[c0:c1] if coords is None else None,
+                             cy[c0:c1] if coords is None else None,
+                             cid[c0:c1] if coords is None else None, coords, seconds, cc_max,
+                             cc_cnt)
+        c0 = c1
 
 
 class Writer:
@@ -147,6 +169,23 @@ class Writer:
                    cc_max, cc_cnt):
         self._submit(1, (out_dir, base, w, conf, rows, n_vert, cx, cy, cid, coords, seconds,
                          cc_max, cc_cnt))
+
+    def group(self, out_dir, items, w, conf, rows, cx, cy, cid):
+        """A group of micrographs (write_group) as one task; a base name already written
+        earlier in the run waits for every pending write first (the reference's order)."""
+        names = [it[0] for it in items]
+        if any(b in self._bases for b in names):
+            self._flush()
+            self._drain()
+        self._bases.update(names)
+        args = (out_dir, items, w, conf, rows, cx, cy, cid)
+        if self._pool is None:
+            write_group(*args)
+            return
+        self._flush()
+        self._futs.append(self._pool.submit(_write_chunk, [(2, args)]))
+        if len(self._futs) > 4 * self.threads:
+            self._drain(len(self._futs) // 2)
 
     def close(self):
         try:

@@ -53,6 +53,42 @@ def test_shard_bounds_balanced():
             assert all(b[i] <= b[i + 1] for i in range(world))
 
 
+def test_shard_bounds_pair_work_skewed_within_one_over_world():
+    """Skewed micrograph list (a few crowded micrographs among many small ones): contiguous
+    shards by pair_work (get_cliques.py:135-138 work per micrograph) are within max item /
+    ideal of a perfect split, i.e. no shard exceeds ideal + the largest single micrograph."""
+    from repic_amd.dist import pair_work, shard_bounds
+    rng = np.random.default_rng(7)
+    for world in (2, 4, 8):
+        for n, crowded in ((2000, 3000), (20000, 1000)):
+            sizes = [[int(v) for v in rng.integers(100, 400, 3)] for _ in range(n)]
+            for i in rng.choice(n, n // 100, replace=False):
+                sizes[i] = [crowded] * 3            # C3-like crowded micrographs (1 %)
+            w = np.array([1.0 + pair_work(s) for s in sizes])
+            b = shard_bounds(w, world)
+            ideal = w.sum() / world
+            loads = [w[b[r]:b[r + 1]].sum() for r in range(world)]
+            # a contiguous split overshoots by at most one micrograph
+            assert max(loads) <= ideal + w.max()
+            if w.max() <= ideal / world:    # items small next to a shard: within 1/world
+                assert max(loads) <= ideal * (1 + 1.0 / world)
+
+
+def test_cli_backend_choice(monkeypatch):
+    """The CLI's collectives: gloo when ranks share a GPU (or none is visible), gloo + RCCL
+    for device tensors when every local rank owns one GPU."""
+    from repic_amd import _lib
+    from repic_amd.commands import get_cliques as gc
+    monkeypatch.setattr(_lib, "device_count", lambda: 8)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert gc._dist_backend(8) == "cpu:gloo,cuda:nccl"
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    monkeypatch.setattr(_lib, "device_count", lambda: 1)
+    assert gc._dist_backend(2) == "gloo"
+    monkeypatch.setattr(_lib, "device_count", lambda: (_ for _ in ()).throw(_lib.RGCError("x")))
+    assert gc._dist_backend(2) == "gloo"
+
+
 CPU_CODE = r"""
 import json, os, torch.distributed as dist
 from repic_amd.dist import exclusive_offsets, reduce_counts, first_failure

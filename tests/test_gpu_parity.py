@@ -26,21 +26,15 @@ def _args(in_dir, out_dir, meta, **kw):
 
 
 def _run_case(name, tmp_path, no_fused=False, **kw):
-    from repic_amd import pipeline
     from repic_amd.commands import get_cliques
-    if no_fused:
-        orig = pipeline.run_batch
-        get_cliques.run_batch = lambda *a, **k_: orig(*a, no_fused=True, **k_)
     meta, data = load_case(name)
     in_dir = make_inputs(name, str(tmp_path))
     out_dir = os.path.join(str(tmp_path), "out")
     exc = None
     try:
-        get_cliques.main(_args(in_dir, out_dir, meta, **kw))
+        get_cliques.main(_args(in_dir, out_dir, meta, no_fused=no_fused, **kw))
     except Exception as e:  # noqa: BLE001 - the exception class is part of the contract
         exc = e
-    finally:
-        get_cliques.run_batch = pipeline.run_batch
     if meta["exception"]:
         assert exc is not None and isinstance(exc, getattr(builtins, meta["exception"])), exc
     else:

@@ -151,6 +151,53 @@ def test_parser_random_floats_roundtrip(tmp_path):
     assert np.array_equal(np.array(vals).view(np.uint64), got.x.view(np.uint64))
 
 
+def _decimal_tokens(rng, n):
+    """Decimal strings of the shapes BOX files hold (fixed point, 1-22 significant digits,
+    leading zeros, signs) plus strings at double rounding midpoints: the decimal expansion of
+    (d1 + d2) / 2 for adjacent doubles, and its neighbours in the last printed digit."""
+    from decimal import Decimal, getcontext
+    getcontext().prec = 60
+    out = []
+    for _ in range(n):
+        r = rng.random()
+        if r < 0.4:
+            out.append(repr(rng.random() * 10 ** rng.randint(-3, 5)))
+        elif r < 0.6:
+            ip = str(rng.randint(0, 10 ** rng.randint(0, 12)))
+            fp = "".join(rng.choice("0123456789") for _ in range(rng.randint(0, 20)))
+            out.append(rng.choice(["", "-", "+"]) + ip + ("." + fp if fp or rng.random() < .3 else ""))
+        elif r < 0.7:
+            out.append(rng.choice(["0.", ".5", "-0.0", "000123.4500", "9007199254740993",
+                                   "18446744073709551615", "12345678901234567890.5",
+                                   "0.000000000000000000000000001", "1" + "0" * 25]))
+        else:
+            d1 = rng.random() * 10 ** rng.randint(-2, 4)
+            d2 = float(np.nextafter(d1, 2 * d1 + 1))
+            mid = (Decimal(d1) + Decimal(d2)) / 2
+            q = format(mid, "f")
+            if len(q.replace("-", "").replace(".", "").lstrip("0")) > 19:
+                q = format(mid.quantize(Decimal(1).scaleb(-rng.randint(15, 19))), "f")
+            last = int(q[-1])
+            for dd in (-1, 0, 1):
+                out.append(q[:-1] + str((last + dd) % 10))
+    return out
+
+
+def test_parser_fast_decimal_path_is_correctly_rounded(tmp_path):
+    """The x87 fast path (box_parse.cpp fast_decimal) must give Python float()'s bits on every
+    token shape it accepts, including decimal strings at or next to double rounding midpoints
+    (where it must defer to strtod)."""
+    rng = random.Random(11)
+    toks = _decimal_tokens(rng, 40000)
+    lines = "".join(f"{t} 1 1 1 0.5\n" for t in toks)
+    p = _write(tmp_path, "d.box", lines)
+    got = parse_many([p])[0]
+    want = np.array([float(t) for t in toks])
+    assert got.exc is None
+    bad = np.nonzero(got.x.view(np.uint64) != want.view(np.uint64))[0]
+    assert len(bad) == 0, [toks[i] for i in bad[:10]]
+
+
 def test_sigmoid_vector_equals_scalar_loop():
     """numpy's vectorised exp gives the same bits as the reference's per-value loop."""
     rng = np.random.default_rng(4)
