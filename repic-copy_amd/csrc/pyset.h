@@ -68,20 +68,36 @@ constexpr uint64_t XXPRIME_1 = 11400714785074694791ULL;
 constexpr uint64_t XXPRIME_2 = 14029467366897019727ULL;
 constexpr uint64_t XXPRIME_5 = 2870177450012600261ULL;
 
+// The multipliers as scalar-register values made inside the caller's loop: left as plain
+// literals, the compiler hoists them into vector registers for the whole fused kernel, where
+// they were spilled to scratch (rgc_fused.hip's order pass runs them rarely).
+#if defined(__HIP_DEVICE_COMPILE__)
+template <uint64_t C>
+__device__ __forceinline__ uint64_t pys_sconst() {
+  uint32_t lo, hi;
+  asm volatile("s_mov_b32 %0, %1" : "=s"(lo) : "i"((uint32_t)(C & 0xFFFFFFFFu)));
+  asm volatile("s_mov_b32 %0, %1" : "=s"(hi) : "i"((uint32_t)(C >> 32)));
+  return ((uint64_t)hi << 32) | lo;
+}
+#define PYS_CONST(C) pys_sconst<C>()
+#else
+#define PYS_CONST(C) (C)
+#endif
+
 PYS_FN uint64_t xx_round(uint64_t acc, uint64_t lane) {
-  acc += lane * XXPRIME_2;
+  acc += lane * PYS_CONST(XXPRIME_2);
   acc = (acc << 31) | (acc >> 33);
-  acc *= XXPRIME_1;
+  acc *= PYS_CONST(XXPRIME_1);
   return acc;
 }
 
 // hash((x, y, id)) — the networkx node key built by add_nodes_to_graph (get_cliques.py:33-34).
 PYS_FN uint64_t hash_node(double x, double y, int64_t id) {
-  uint64_t acc = XXPRIME_5;
+  uint64_t acc = PYS_CONST(XXPRIME_5);
   acc = xx_round(acc, hash_double(x));
   acc = xx_round(acc, hash_double(y));
   acc = xx_round(acc, hash_id(id));
-  acc += 3ULL ^ (XXPRIME_5 ^ 3527539ULL);
+  acc += PYS_CONST(3ULL ^ (XXPRIME_5 ^ 3527539ULL));
   if (acc == (uint64_t)-1) return 1546275796ULL;
   return acc;
 }

@@ -1450,9 +1450,10 @@ int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) 
   TRY(rounds(1, 1 << 20));
   TRY(rounds(2, 1 << 16));
   rgc::launch_ilp_cert(s, 3, A);
-  // projected subgradient iterations of the Lagrangian bound (per component Polyak steps,
-  // halved after 8 iterations without progress: 300 halve mu up to ~37 times)
-  for (int it = 0; it < 300; ++it) rgc::launch_ilp_cert(s, 4, A);
+  // projected subgradient iterations of the Lagrangian bound (per component Polyak steps
+  // towards the primal; after 20 iterations without progress the step halves and lam
+  // restarts from the best one)
+  for (int it = 0; it < 1000; ++it) rgc::launch_ilp_cert(s, 4, A);
   rgc::launch_ilp_cert(s, 5, A);
   TRY(mark(c, "d2h_x"));
   HIPCHK(hipGetLastError());

@@ -132,6 +132,7 @@ struct FCtx {
   // copies of the kernel arguments (taking the address of the kernarg struct would move it
   // to scratch)
   double B, two_b2;
+  float Bf, two_b2f;   // (float) copies, wave-uniform (SGPRs)
   int flags;
   const double* score;
   int32_t* rows;
@@ -253,6 +254,12 @@ __device__ __forceinline__ double ufd(double v) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+__device__ __forceinline__ int64_t ufl64(int64_t v) {
+  const int lo = __builtin_amdgcn_readfirstlane((int)(v & 0xFFFFFFFF));
+  const int hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
 // the micrograph's grid geometry, uniform across the workgroup
 struct GridU {
   double minx, miny, inv_cell;
@@ -355,8 +362,8 @@ __device__ __forceinline__ bool fused_epilogue_main(const FCtx<K>& c, int64_t j,
 #pragma unroll
         for (int b = a + 1; b < K; ++b) {
           if constexpr (INTP) {
-            const float Bf = (float)c.B;
-            I[t++] = fmaxf(Bf - fabsf(xs[a] - xs[b]), 0.0f) * fmaxf(Bf - fabsf(ys[a] - ys[b]), 0.0f);
+            I[t++] = fmaxf(c.Bf - fabsf(xs[a] - xs[b]), 0.0f) *
+                     fmaxf(c.Bf - fabsf(ys[a] - ys[b]), 0.0f);
           } else {
             I[t++] = overlap(xs[a], ys[a], xs[b], ys[b], c.B);
           }
@@ -412,7 +419,7 @@ __device__ __forceinline__ bool fused_epilogue_main(const FCtx<K>& c, int64_t j,
 #pragma unroll
       for (int b = a + 1; b < K; ++b) {
         float jf;
-        if constexpr (INTP) jf = I[t] * __builtin_amdgcn_rcpf((float)c.two_b2 - I[t]);
+        if constexpr (INTP) jf = I[t] * __builtin_amdgcn_rcpf(c.two_b2f - I[t]);
         else jf = (float)I[t] * __builtin_amdgcn_rcpf((float)(c.two_b2 - I[t]));
         deg[a] += jf;
         deg[b] += jf;
@@ -619,9 +626,9 @@ struct BfsLevel {
       CN[e] = cnt;
     }
     __syncthreads();
-    const int64_t nN = block_scan_dpp<NT>(CN, (int)nD, H.red64);
+    const int64_t nN = ufl64(block_scan_dpp<NT>(CN, (int)nD, H.red64));
     constexpr bool last = D + 1 == K;
-    const int nb = (lvl[D] + 4 * (int)nD + 3) & ~3;   // next level starts here
+    const int nb = ufl((lvl[D] + 4 * (int)nD + 3) & ~3);   // next level starts here
     if (K >= 4) {
       const float f = fminf(bfs_fit(nN, 65535), bfs_fit(nN * (last ? 6 : 4), tb - nb));
       out.fit = fminf(out.fit, f);
@@ -702,7 +709,7 @@ __device__ __forceinline__ BfsOut<K> bfs_cliques(const FShared& S, FusedHdr& H, 
     cnt[i] = root_ok(r) ? (uint32_t)(seg_end(r) - S.fwd[r]) : 0u;
   }
   __syncthreads();
-  const int64_t n2 = block_scan_dpp<NT>(cnt, nr, H.red64);
+  const int64_t n2 = ufl64(block_scan_dpp<NT>(cnt, nr, H.red64));
   constexpr bool last = K == 2;
   if (K >= 4) out.fit = fminf(bfs_fit(n2, 65535), bfs_fit(n2 * (last ? 6 : 4), qbytes));
   if (n2 > 65535 || n2 * (last ? 6 : 4) > qbytes) {
@@ -1025,6 +1032,8 @@ void k_fused(FusedArgs A) {
   STAMP(0);
   FCtx<K> c;
   c.B = A.B; c.two_b2 = A.two_b2; c.flags = A.flags; c.score = A.score;
+  c.Bf = uff((float)A.B);
+  c.two_b2f = uff((float)A.two_b2);
   c.rows = A.rows; c.w = A.w; c.conf = A.conf; c.consensus = A.consensus;
   c.members = A.members; c.order = A.order;
   c.S = S;

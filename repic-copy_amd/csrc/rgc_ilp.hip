@@ -481,7 +481,7 @@ __global__ __launch_bounds__(64) void k_ilp_wave(IlpArgs A, int n_big) {
 //   * RGC_ILP_GAP_OK when lbest - primal <= 1e-4 primal, else the packing with status
 //     NODE_LIMIT / HEURISTIC.
 constexpr uint8_t ST_UND = 0, ST_IN = 1, ST_OUT = 2, ST_NONE = 3;
-constexpr int CS = 8;   // doubles per component record: lsum g2 lbest mu primal step stall pad
+constexpr int CS = 8;   // doubles per component record: lsum g2 lbest mu primal step stall flag
 
 __device__ __forceinline__ int64_t ilp_comp(const IlpArgs& A, int64_t c) {
   return A.comp_id[A.parent[c]];
@@ -501,6 +501,7 @@ __global__ __launch_bounds__(ILP_WG) void k_cert_flag(IlpArgs A) {
   A.cert[comp] = f;
   double* cs = A.cs + comp * CS;
   cs[0] = 0.0; cs[1] = 0.0; cs[2] = INFINITY; cs[3] = 2.0; cs[4] = 0.0; cs[5] = 0.0; cs[6] = 0.0;
+  cs[7] = 0.0;
 }
 
 // per column: priority key and state; chosen columns of node-limit components own their rows
@@ -660,13 +661,20 @@ __global__ __launch_bounds__(ILP_WG) void k_lr_step(IlpArgs A) {
   if (comp >= A.n_comp || A.cert[comp] == 0) return;
   double* cs = A.cs + comp * CS;
   const double L = cs[0], g2 = cs[1], P = cs[4];
-  if (L < cs[2]) {
-    if (L < cs[2] - 1e-9 * fabs(cs[2])) cs[6] = 0.0; else cs[6] += 1.0;
-    cs[2] = L;
+  // cs[7]: 1 = this lam is the best so far (rows keep a copy), 2 = restart from that copy
+  cs[7] = 0.0;
+  if (!(L >= cs[2] - 1e-9 * fabs(cs[2]))) {   // (first iteration: cs[2] = inf)
+    cs[2] = fmin(cs[2], L);
+    cs[6] = 0.0;
+    cs[7] = 1.0;
   } else {
     cs[6] += 1.0;
   }
-  if (cs[6] >= 8.0) { cs[3] *= 0.5; cs[6] = 0.0; }
+  if (cs[6] >= 20.0) {          // no progress: halve the step, restart from the best lam
+    cs[3] *= 0.5;
+    cs[6] = 0.0;
+    cs[7] = 2.0;
+  }
   cs[5] = g2 > 0.0 ? cs[3] * fmax(L - P, 0.0) / g2 : 0.0;
   cs[0] = 0.0;
   cs[1] = 0.0;
@@ -676,7 +684,12 @@ __global__ __launch_bounds__(ILP_WG) void k_lr_lam(IlpArgs A) {
   if (r >= A.n_rows) return;
   const int64_t comp = ilp_row_comp(A, r);
   if (comp < 0 || A.cert[comp] == 0) return;
-  A.lam[r] = fmax(0.0, A.lam[r] - A.cs[comp * CS + 5] * A.grad[r]);
+  const double* cs = A.cs + comp * CS;
+  // the best lam lives in rmax (the claims are dead by now) as double bits
+  double* best = reinterpret_cast<double*>(A.rmax);
+  if (cs[7] == 1.0) best[r] = A.lam[r];
+  if (cs[7] == 2.0) A.lam[r] = best[r];
+  else A.lam[r] = fmax(0.0, A.lam[r] - cs[5] * A.grad[r]);
   A.grad[r] = 0.0;
 }
 // x and the component statuses
