@@ -49,7 +49,7 @@ struct FusedHdr {
     double red4[4][MAXW];
   };
   int nonint[MAXW];   // P0: per wave, some finite coordinate is not an integer in (-2^23, 2^23)
-  double minx, miny, cell, inv_cell;
+  double minx, miny, cell, inv_cell, inv_celly;
   double xbs;       // P5 x-bucket scale: bucket(x) = min(trunc((x - minx) * xbs), n - 1)
   float inv_gy;
   int gx, gy, ncell, nkey;   // per-picker grid gx x gy; keys picker * ncell + cell; nkey = none
@@ -262,13 +262,15 @@ __device__ __forceinline__ int64_t ufl64(int64_t v) {
 
 // the micrograph's grid geometry, uniform across the workgroup
 struct GridU {
-  double minx, miny, inv_cell;
+  double minx, miny, inv_cell, inv_celly;   // columns >= 1.08 B wide, rows >= 0.54 B tall
+  float inv_cellf;                          // (float)inv_cell: P2's half-column test
   float inv_gy;
   int gx, gy, ncell, nkey;
 };
 __device__ __forceinline__ GridU grid_u(const FusedHdr& H) {
   GridU G;
   G.minx = ufd(H.minx); G.miny = ufd(H.miny); G.inv_cell = ufd(H.inv_cell);
+  G.inv_celly = ufd(H.inv_celly); G.inv_cellf = uff((float)H.inv_cell);
   G.inv_gy = uff(H.inv_gy);
   G.gx = ufl(H.gx); G.gy = ufl(H.gy); G.ncell = ufl(H.ncell); G.nkey = ufl(H.nkey);
   return G;
@@ -279,7 +281,7 @@ __device__ __forceinline__ GridU grid_u(const FusedHdr& H) {
 __device__ __forceinline__ int box_key(const GridU& H, int p, double x, double y) {
   if (H.ncell == 0 || !isfinite(x) || !isfinite(y)) return H.nkey;
   const int cx = (int)fmin(floor((x - H.minx) * H.inv_cell), (double)(H.gx - 1));
-  const int cy = (int)fmin(floor((y - H.miny) * H.inv_cell), (double)(H.gy - 1));
+  const int cy = (int)fmin(floor((y - H.miny) * H.inv_celly), (double)(H.gy - 1));
   return p * H.ncell + cx * H.gy + cy;
 }
 
@@ -743,8 +745,10 @@ __device__ __forceinline__ BfsOut<K> bfs_cliques(const FShared& S, FusedHdr& H, 
   }
 }
 
-// Candidates of a box: the 3x3 cell stencil around its cell in the grid of every HIGHER
-// picker (forward edges only), i.e. up to 3 (K - 1 - p) column ranges of sorted positions.
+// Candidates of a box: the 2x3 cell stencil at its cell in the grid of every HIGHER picker
+// (forward edges only): columns cx, cx + 1 from cx = its column - 1 or its column (by the
+// half of the column the box lies in), rows y0..y1, i.e. up to 2 (K - 1 - p) ranges of
+// sorted positions.
 struct Stencil {
   int p, cx, y0, y1;   // p = K: no candidates
   double2 a;
@@ -770,13 +774,15 @@ __device__ __forceinline__ void stencil_setup(Stencil& st, int ts, const FShared
   cx += ((cx + 1) * gy <= cell) ? 1 : 0;
   cx -= (cx * gy > cell) ? 1 : 0;
   const int cy = cell - cx * gy;
+  // half-column test in f32 (0.0014 columns of slack, see P1): left half -> columns cx-1, cx
+  const float u = (float)(st.a.x - H.minx) * H.inv_cellf;
   st.p = p;
-  st.cx = cx;
+  st.cx = cx - ((u - (float)cx) < 0.5f ? 1 : 0);
   st.y0 = max(cy - 1, 0);
   st.y1 = min(cy + 1, gy - 1);
 }
 
-// column range [lo, hi) of the stencil in picker q's grid, column offset d (-1, 0, 1)
+// column range [lo, hi) of the stencil in picker q's grid, column st.cx + d (d = 0, 1)
 __device__ __forceinline__ void stencil_range(const Stencil& st, const FShared& S,
                                               const GridU& H, int q, int d, int& lo, int& hi) {
   const int col = st.cx + d;
@@ -816,13 +822,14 @@ __device__ __forceinline__ bool edge_test(double2 a, double2 b, double B, double
 }
 
 // P2 count for the box at sorted position ts (thread per box): JI test against every stencil
-// candidate of a higher picker; returns the edge count and the bitmask of edge candidates
-// (candidates 0..31 in stencil order; later candidates are re-tested by the fill).
+// candidate of a higher picker; returns the edge count and, for the fill, either the targets
+// themselves (at most 2 edges: first << 16 | second, ascending) or the bitmask of edge
+// candidates (candidates 0..31 in stencil order; later candidates are re-tested by the fill).
 template <int K, bool W>
 __device__ __forceinline__ int pairs_count(const Stencil& st, const FShared& S, const GridU& H,
                                            double B, double two_b2, double i_lo, double i_hi,
                                            uint32_t* mask_out) {
-  uint32_t mask = 0;
+  uint32_t mask = 0, pk = 0;
   int cnt = 0, kk = 0;
   // f32 layout: reject in f32 first.  An edge needs both overlaps > (6/13) B, i.e. |dx| and
   // |dy| < (7/13) B = 0.5385 B; the f32 difference of two exact f32 values is within 2^-24 of
@@ -831,7 +838,7 @@ __device__ __forceinline__ int pairs_count(const Stencil& st, const FShared& S, 
   const float ax = (float)st.a.x, ay = (float)st.a.y;
   for (int q = st.p + 1; q < K; ++q) {
 #pragma unroll
-    for (int d = -1; d <= 1; ++d) {
+    for (int d = 0; d <= 1; ++d) {
       int lo, hi;
       stencil_range(st, S, H, q, d, lo, hi);
       for (int t = lo; t < hi; ++t, ++kk) {
@@ -848,11 +855,12 @@ __device__ __forceinline__ int pairs_count(const Stencil& st, const FShared& S, 
         if (e) {
           ++cnt;
           mask |= (kk < 32) ? (1u << kk) : 0u;
+          pk = (pk << 16) | (uint32_t)t;
         }
       }
     }
   }
-  *mask_out = mask;
+  *mask_out = cnt <= 2 ? pk : mask;
   return cnt;
 }
 
@@ -861,22 +869,22 @@ template <int K>
 __device__ __forceinline__ int pairs_count_int(const Stencil& st, const FShared& S,
                                                const GridU& H, float Bf, float Tf,
                                                uint32_t* mask_out) {
-  uint32_t mask = 0;
+  uint32_t mask = 0, pk = 0;
   int cnt = 0, kk = 0;
   const float ax = (float)st.a.x, ay = (float)st.a.y;
 #ifdef RGC_X_P2A
   // every stencil range of every higher picker first (one batch of LDS reads), then one
   // non-unrolled candidate loop per range
-  constexpr int NR = 3 * (K - 1);
+  constexpr int NR = 2 * (K - 1);
   int lo[NR], hi[NR];
 #pragma unroll
   for (int qi = 0; qi < K - 1; ++qi)
 #pragma unroll
-    for (int d = 0; d < 3; ++d) {
+    for (int d = 0; d < 2; ++d) {
       int l = 0, h = 0;
-      if (qi + 1 > st.p) stencil_range(st, S, H, qi + 1, d - 1, l, h);
-      lo[qi * 3 + d] = l;
-      hi[qi * 3 + d] = h;
+      if (qi + 1 > st.p) stencil_range(st, S, H, qi + 1, d, l, h);
+      lo[qi * 2 + d] = l;
+      hi[qi * 2 + d] = h;
     }
 #pragma unroll
   for (int r = 0; r < NR; ++r) {
@@ -888,13 +896,14 @@ __device__ __forceinline__ int pairs_count_int(const Stencil& st, const FShared&
       if (xo * yo > Tf) {
         ++cnt;
         mask |= (kk < 32) ? (1u << kk) : 0u;
+        pk = (pk << 16) | (uint32_t)t;
       }
     }
   }
 #else
   for (int q = st.p + 1; q < K; ++q) {
 #pragma unroll
-    for (int d = -1; d <= 1; ++d) {
+    for (int d = 0; d <= 1; ++d) {
       int lo, hi;
       stencil_range(st, S, H, q, d, lo, hi);
       for (int t = lo; t < hi; ++t, ++kk) {
@@ -904,12 +913,13 @@ __device__ __forceinline__ int pairs_count_int(const Stencil& st, const FShared&
         if (xo * yo > Tf) {
           ++cnt;
           mask |= (kk < 32) ? (1u << kk) : 0u;
+          pk = (pk << 16) | (uint32_t)t;
         }
       }
     }
   }
 #endif
-  *mask_out = mask;
+  *mask_out = cnt <= 2 ? pk : mask;
   return cnt;
 }
 
@@ -923,7 +933,7 @@ __device__ __forceinline__ void pairs_fill(const Stencil& st, const FShared& S, 
   int c = 0, kk = 0;
   for (int q = st.p + 1; q < K; ++q) {
 #pragma unroll
-    for (int dd = -1; dd <= 1; ++dd) {
+    for (int dd = 0; dd <= 1; ++dd) {
       int lo, hi;
       stencil_range(st, S, H, q, dd, lo, hi);
       const int len = hi - lo;
@@ -1123,17 +1133,21 @@ void k_fused(FusedArgs A) {
   STAMP(1);
   // ---- P1: one grid per picker (x-major cells, K * gx * gy <= 4 nmax + 4 cells in all) and
   // an LDS counting sort of the boxes by (picker, cell).  JI > 0.3 implies I > (6/13) B^2 and
-  // so |dx|, |dy| < (7/13) B = 0.5385 B: cells of side >= 0.54 B keep every edge inside the
-  // 3x3 stencil, and per-picker grids let a box visit the boxes of higher pickers only.
+  // so |dx|, |dy| < (7/13) B = 0.5385 B: with cells >= 1.08 B wide and >= 0.54 B tall every
+  // edge partner lies in the box's own column or the neighbouring column on the side of the
+  // box's half of its column (its x is within 0.4986 columns), three rows around its row: a
+  // 2x3 stencil, i.e. two contiguous position ranges per grid.  Per-picker grids let a box
+  // visit the boxes of higher pickers only.
   // the grid is planned by every thread from the reduced bounding box (identical values, no
   // thread-0 section and barrier); thread 0 only records what later phases read.  Planned in
   // f32 with hardware reciprocals (every wave pays for it): exactness is not needed, only
-  // cells >= 0.54 B (0.28 % above the 7/13 B an edge needs, far above f32 rounding), K gx gy
-  // within the budget (checked on the integers used), and one inv_cell used by every key.
+  // cells >= 1.08 B x 0.54 B (0.28 % above what an edge needs, far above f32 rounding; the
+  // half-column test has 0.0014 columns of slack), K gx gy within the budget (checked on the
+  // integers used), and one inv_cell / inv_celly used by every key.
   GridU G;
   double xbs;
   {
-    double cl = A.B, icl = 0.0;
+    double cl = A.B, icl = 0.0, icly = 0.0;
     int gx = 0, gy = 0;
     if (mnx <= mxx && A.B > 0.0) {
       const double ex = mxx - mnx, ey = mxy - mny;
@@ -1142,31 +1156,37 @@ void k_fused(FusedArgs A) {
       } else {
         const int budget = (fused_cells(A.nmax) + 4) / K;
         const float fex = (float)ex, fey = (float)ey, rb = __builtin_amdgcn_rcpf((float)budget);
-        float fcl = fmaxf((float)(0.54 * A.B) * 1.000001f,
-                          fmaxf(__builtin_sqrtf(fex * fey * rb), fmaxf(fex, fey) * rb));
+        // row height h, column width 2 h
+        float fch = fmaxf((float)(0.54 * A.B) * 1.000001f,
+                          fmaxf(__builtin_sqrtf(0.5f * fex * fey * rb),
+                                fmaxf(0.5f * fex, fey) * rb));
         for (;;) {
-          const float ir = __builtin_amdgcn_rcpf(fcl);
-          const int fx = (int)floorf(fex * ir) + 1, fy = (int)floorf(fey * ir) + 1;
+          const float iry = __builtin_amdgcn_rcpf(fch);
+          const int fx = (int)floorf(fex * (0.5f * iry)) + 1, fy = (int)floorf(fey * iry) + 1;
           if (fx <= budget && fy <= budget && fx * fy <= budget) {
             gx = fx; gy = fy;
             break;
           }
-          fcl *= 1.0625f;
+          fch *= 1.0625f;
         }
-        cl = (double)fcl;
-        icl = (double)__builtin_amdgcn_rcpf(fcl);
-        // keys use icl: a cell is 1 / icl wide, which must stay >= 0.54 B
-        if (icl * (0.54 * A.B) > 1.0) icl = 1.0 / (0.54 * A.B);
+        cl = (double)fch;
+        icly = (double)__builtin_amdgcn_rcpf(fch);
+        icl = 0.5 * icly;
+        // keys use icl / icly: columns must stay >= 1.08 B wide, rows >= 0.54 B tall
+        if (icl * (1.08 * A.B) > 1.0) icl = 1.0 / (1.08 * A.B);
+        if (icly * (0.54 * A.B) > 1.0) icly = 1.0 / (0.54 * A.B);
       }
     }
-    G.minx = ufd(mnx); G.miny = ufd(mny); G.inv_cell = ufd(icl);
+    G.minx = ufd(mnx); G.miny = ufd(mny); G.inv_cell = ufd(icl); G.inv_celly = ufd(icly);
+    G.inv_cellf = uff((float)icl);
     G.gx = ufl(gx); G.gy = ufl(gy); G.ncell = G.gx * G.gy; G.nkey = K * G.ncell;
     G.inv_gy = G.gy > 0 ? __builtin_amdgcn_rcpf((float)G.gy) : 0.0f;
     const double ex = mxx - mnx;
     xbs = ufd((mnx < mxx && ex < 0x1p60) ? (double)((float)n * __builtin_amdgcn_rcpf((float)ex))
                                          : 0.0);
     if (tid == 0) {
-      H.minx = mnx; H.miny = mny; H.cell = cl; H.inv_cell = icl; H.gx = G.gx; H.gy = G.gy;
+      H.minx = mnx; H.miny = mny; H.cell = cl; H.inv_cell = icl; H.inv_celly = icly;
+      H.gx = G.gx; H.gy = G.gy;
       H.ncell = G.ncell; H.nkey = G.nkey; H.inv_gy = G.inv_gy; H.xbs = xbs;
       H.status = 0; H.C = 0; H.base = 0; H.V = 0; H.target = -1; H.ccur = 0;
       H.tief[0] = H.tief[1] = 0;
@@ -1239,7 +1259,7 @@ void k_fused(FusedArgs A) {
   // thread per box (sorted position): lanes of a wave hold neighbouring boxes of one picker,
   // so their stencils overlap (similar trip counts, broadcast LDS reads), and the waves of
   // picker K-1 have nothing to do.  cnt[] (dead until P3) keeps
-  // each box's edge bitmask for the fill.
+  // each box's targets (<= 2 edges) or edge bitmask for the fill.
   uint32_t* ccsz = reinterpret_cast<uint32_t*>(S.vrank);   // packed u16 CC sizes (P2-P3)
   // boustrophedon box order: odd rounds walk their FWG positions backwards, so a thread that
   // took a low-picker box (most grids to search) in one round takes a high-picker box (fewest)
@@ -1279,10 +1299,16 @@ void k_fused(FusedArgs A) {
       const int i = ts;
       const int base = S.fwd[i], cnt = (int)S.fwd[i + 1] - base;
       if (cnt == 0) continue;
-      Stencil st;
-      stencil_setup<K, W>(st, ts, S, G);
       uint16_t* d = S.dst + base;
-      pairs_fill<K, W>(st, S, G, S.cnt[ts], d, cnt, B, two_b2, i_lo, i_hi);
+      const uint32_t cw0 = S.cnt[ts];
+      if (cnt <= 2) {   // the count kept the targets themselves (ascending)
+        d[0] = (uint16_t)(cnt == 2 ? cw0 >> 16 : cw0);
+        if (cnt == 2) d[1] = (uint16_t)cw0;
+      } else {
+        Stencil st;
+        stencil_setup<K, W>(st, ts, S, G);
+        pairs_fill<K, W>(st, S, G, cw0, d, cnt, B, two_b2, i_lo, i_hi);
+      }
       S.flags[i] = 1;
       if (src_ok) {
         for (int e = 0; e < cnt; ++e) esrc[base + e] = (uint16_t)i;

@@ -17,6 +17,24 @@ from scipy.sparse import coo_matrix
 
 from golden_util import load_case
 
+_HIGHS = None
+
+
+def highs(A, w):
+    """HiGHS optimum (x uint8, objective) of the model: from tests/golden/ilp_highs.npz
+    (make_ilp_golden.py, keyed by the model's sha256) when present, else a live solve."""
+    global _HIGHS
+    import make_ilp_golden
+    from oracle import ilp_ref
+    if _HIGHS is None:
+        _HIGHS = make_ilp_golden.load()
+    hit = _HIGHS.get(make_ilp_golden.model_key(A, w))
+    if hit is None:
+        return ilp_ref.milp(A, w)
+    x = np.zeros(A.shape[1], np.uint8)
+    x[hit[1]] = 1
+    return x, hit[0]
+
 
 def golden_problems(name="c1_10017"):
     meta, data = load_case(name)
@@ -64,6 +82,25 @@ def test_milp_oracle_matches_brute_force_on_golden():
     assert n >= 6
 
 
+def test_highs_fixture_matches_live_solves():
+    """The committed HiGHS optima (make_ilp_golden.py) cover every model the GPU tests solve
+    and agree with live solves on the golden micrographs."""
+    import make_ilp_golden
+    from oracle import ilp_ref
+    tab = make_ilp_golden.load()
+    probs = golden_problems() + golden_problems("syn_k4") + golden_problems("syn_k5")
+    for A, w in probs:
+        obj, sel = tab[make_ilp_golden.model_key(A, w)]
+        x, objr = ilp_ref.milp(A, w)
+        assert abs(obj - objr) <= 1e-12 * max(1.0, objr)
+        xs = np.zeros(A.shape[1], np.uint8)
+        xs[sel] = 1
+        assert ilp_ref.is_packing(A, xs)
+        assert abs(float(np.asarray(w, np.float64)[sel].sum()) - obj) <= 1e-9 * max(1.0, obj)
+    for A, w in synthetic_problems("C3", 3) + _c5_window_problems(640, 2):
+        assert make_ilp_golden.model_key(A, w) in tab
+
+
 def _check(problems, xs, exact, inexact_gap=None):
     """Exact components must reach the optimum; with ``inexact_gap`` a micrograph whose solve
     hit the node limit must be a packing within that relative gap of it."""
@@ -73,7 +110,7 @@ def _check(problems, xs, exact, inexact_gap=None):
         assert ilp_ref.is_packing(A, x)
         w64 = np.asarray(w, np.float64)
         obj = float(np.sum(w64[x == 1]))
-        xr, objr = ilp_ref.milp(A, w)
+        xr, objr = highs(A, w)
         if not ex:
             assert inexact_gap is not None
             gaps.append((objr - obj) / objr)
@@ -138,7 +175,7 @@ def test_gpu_run_ilp_cli_on_get_cliques_output(tmp_path):
         ld = lambda s: pickle.load(open(os.path.join(out, base + s), "rb"))  # noqa: E731
         A, w = ld("_constraint_matrix.pickle"), ld("_weight_vector.pickle")
         coords, conf = ld("_consensus_coords.pickle"), ld("_consensus_confidences.pickle")
-        x, _ = ilp_ref.milp(A, w)
+        x, _ = highs(A, w)
         want = sorted(((int(np.rint(coords[j][0])), int(np.rint(coords[j][1])), str(conf[j]))
                        for j in np.flatnonzero(x)), key=lambda t: (-float(t[2]), t))
         got = [ln.split("\t") for ln in open(os.path.join(out, base + ".box")).read().splitlines()]
@@ -221,7 +258,7 @@ def test_gpu_ilp_large_component_certified_against_highs():
         assert s in (GAP_OK, HEURISTIC)
         w64 = np.asarray(w, np.float64)
         obj = float(w64[x == 1].sum())
-        _, objr = ilp_ref.milp(A, w)
+        _, objr = highs(A, w)
         gap = (objr - obj) / objr
         print("C5 window: cliques", len(w), "status", s, "gap vs HiGHS", gap)
         assert gap >= -1e-12
@@ -244,7 +281,7 @@ def test_gpu_ilp_node_limit_components_certified():
     for (A, w), x, s in zip(probs, xs, st):
         assert ilp_ref.is_packing(A, x)
         obj = float(np.asarray(w, np.float64)[x == 1].sum())
-        _, objr = ilp_ref.milp(A, w)
+        _, objr = highs(A, w)
         gap = (objr - obj) / objr
         print("C3: status", s, "gap vs HiGHS", gap)
         assert s in (OPTIMAL, GAP_OK, NODE_LIMIT)
