@@ -101,6 +101,59 @@ __device__ __forceinline__ T wave_incl_scan(T v, Op op) {
   return v;
 }
 
+// 32-bit inclusive add / max scans across the wave (lane 63: the total) with the DPP moves'
+// bound_ctrl / row_mask: lanes without a source lane read 0, so every step is one move and
+// one unconditional op (max: non-negative values only)
+__device__ __forceinline__ int dpp_shr_add(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);   // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+__device__ __forceinline__ int wave_incl_add32(int v) { return dpp_shr_add(v); }
+__device__ __forceinline__ int wave_incl_max32(int v) {
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));
+  return v;
+}
+
+// In-place exclusive scan of a[0..n) in LDS whose total fits 31 bits (u16 arrays: boxes,
+// edges, vertices), a[n] = total, on 32-bit DPP wave scans; same barriers and contract as
+// block_scan_dpp below (lds: BS / 64 ints).
+template <int BS, typename A>
+__device__ __forceinline__ int block_scan_dpp32(A* a, int n, int* lds) {
+  const int per = (n + BS - 1) / BS;
+  const int c0 = min((int)threadIdx.x * per, n), c1 = min(c0 + per, n);
+  int s = 0;
+  for (int c = c0; c < c1; ++c) s += a[c];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int inc = wave_incl_add32(s);
+  if (l == 63) lds[w] = inc;
+  __syncthreads();
+  int pre = inc - s, tot = 0;
+#pragma unroll
+  for (int i = 0; i < BS / 64; ++i) {
+    const int x = lds[i];
+    pre += (i < w) ? x : 0;
+    tot += x;
+  }
+  for (int c = c0; c < c1; ++c) {
+    const int v = a[c];
+    a[c] = (A)pre;
+    pre += v;
+  }
+  if (threadIdx.x == BS - 1) a[n] = (A)tot;
+  __syncthreads();
+  return tot;
+}
+
 // Exclusive scan of one value per thread across the workgroup on DPP wave scans.  ONE barrier:
 // the caller guarantees a barrier between any earlier use of lds and this call.
 template <int BS, typename T>

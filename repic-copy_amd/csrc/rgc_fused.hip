@@ -1205,7 +1205,7 @@ void k_fused(FusedArgs A) {
     atomicAdd(&cw[q >> 1], 1u << (16 * (q & 1)));
   });
   __syncthreads();
-  block_scan_dpp<FWG>(S.cstart, nk + 2, H.red64);
+  block_scan_dpp32<FWG>(S.cstart, nk + 2, H.redi);
   // arrival order into fwd (free until P2), made deterministic by the placement pass
   uint16_t* arrival = S.fwd;
   each_box([&](int i, double, double) {
@@ -1278,15 +1278,17 @@ void k_fused(FusedArgs A) {
   }
   __syncthreads();
   STAMP(3);   // count
+  STOP_AFTER(21);
   
   // fwd[n] = E is written by the scan; the status is the same in every thread
-  const int E = (int)block_scan_dpp<FWG>(S.fwd, n, H.red64);
+  const int E = block_scan_dpp32<FWG>(S.fwd, n, H.redi);
   const int st2 = E == 0 ? RGC_ST_NO_EDGES : (E > A.ecap ? RGC_ST_DEFER : 0);
   if (tid == 0) {
     H.E = E;
     H.status = st2;
   }
   STAMP(4);   // scan
+  STOP_AFTER(22);
   if (st2 == 0) {
     // fill each list (already sorted: position order) and record each edge's source in dst's
     // unused tail when it has room; then union the edges one thread per edge (lock-free
@@ -1321,6 +1323,7 @@ void k_fused(FusedArgs A) {
     }
     __syncthreads();
     STAMP(5);   // fill
+    STOP_AFTER(23);
     if (src_ok) {
       for (int e = tid; e < E; e += FWG) {
         const uint32_t h = S.dst[e];
@@ -1373,25 +1376,29 @@ void k_fused(FusedArgs A) {
   {
     // nodes and roots packed in one 64-bit sum, the largest size in one max; every thread
     // reads the per-wave partials (no thread-0 section and second barrier)
-    int64_t nr = 0;
+    // nodes << 16 | roots (both <= n < 2^16) in one 32-bit sum
+    int nr = 0;
     int mx = 0;
     for (int i = tid; i < n; i += FWG) {
       if (S.flags[i]) {
-        nr += 1LL << 32;
+        nr += 1 << 16;
         if (S.parent[i] == (uint32_t)i) { nr += 1; mx = max(mx, cc_size(i)); }
       }
     }
-    nr = wave_incl_scan(nr, [](int64_t a, int64_t b) { return a + b; });
-    mx = wave_incl_scan(mx, [](int a, int b) { return max(a, b); });
-    if ((tid & 63) == 63) { H.red64[tid >> 6] = nr; H.redi[tid >> 6] = mx; }
+    nr = wave_incl_add32(nr);
+    mx = wave_incl_max32(mx);
+    if ((tid & 63) == 63) { H.redi[tid >> 6] = nr; reinterpret_cast<int*>(H.redu)[tid >> 6] = mx; }
     __syncthreads();
-    int64_t t = 0;
+    int t = 0;
     int m2 = 0;
 #pragma unroll
-    for (int w = 0; w < FNW; ++w) { t += H.red64[w]; m2 = max(m2, H.redi[w]); }
-    nodes = (int)(t >> 32);
+    for (int w = 0; w < FNW; ++w) {
+      t += H.redi[w];
+      m2 = max(m2, reinterpret_cast<const int*>(H.redu)[w]);
+    }
+    nodes = t >> 16;
     cc_max = m2;
-    if (tid == 0) { H.nodes = nodes; H.cc_cnt = (int)(t & 0xFFFFFFFF); H.cc_max = cc_max; }
+    if (tid == 0) { H.nodes = nodes; H.cc_cnt = t & 0xFFFF; H.cc_max = cc_max; }
   }
   // (no barrier: the P4 passes below start with their own before touching the reduction
   // slots, and no array read here is written before it)
@@ -1554,7 +1561,7 @@ void k_fused(FusedArgs A) {
       S.vrank[t] = (uint16_t)((atomicAdd(&bw[q >> 1], 1u << sh) >> sh) & 0xFFFFu);
     }
     __syncthreads();
-    const int64_t V = block_scan_dpp<FWG>(bcnt, n, H.red64);
+    const int V = block_scan_dpp32<FWG>(bcnt, n, H.redi);
     if (tid == 0) { H.V = (int)V; bcnt[n] = (uint16_t)V; }
     for (int t = tid; t < n; t += FWG) {
       if (S.flags[t] != 3) continue;

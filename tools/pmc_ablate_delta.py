@@ -12,7 +12,12 @@ for line in open(sys.argv[1]):
         d[cur] = {}
     elif cur and "avg=" in line:
         d[cur][line.split()[0]] = float(line.split("avg=")[1])
-order = sorted(k for k in d if "stop" in k) + ["librepic_gc"]
+def _phase(name):   # stopN; two-digit N = sub-phase N % 10 of phase N // 10 (stop21 < stop2)
+    v = int(name.split("stop")[1])
+    return v if v < 10 else (v // 10 - 1) + (v % 10) / 10
+
+
+order = sorted((k for k in d if "stop" in k), key=_phase) + ["librepic_gc"]
 keys = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
         "SQ_LDS_BANK_CONFLICT")
 print(f"{'phase':22s}" + "".join(f"{k[3:]:>16s}" for k in keys) + "   (millions, marginal)")
