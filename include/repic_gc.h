@@ -8,6 +8,8 @@
  * reference's per-micrograph loop (get_cliques.py:108-229):
  *
  *   rgc_parse_files  <- common.py:71-114 get_box_coords (BOX text -> x, y, score)
+ *   rgc_write_outputs <- get_cliques.py:204-229 (the four pickles + runtime.tsv of each
+ *                       micrograph; ABI 5)
  *   rgc_run          <- get_cliques.py:134-202: Jaccard pairs (:40-69,:134-138), graph
  *                       (:30-37,:142-143), connected components (:145-156), size-k
  *                       cliques (:49-56,:160-161), ILP weight / confidence / consensus
@@ -26,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RGC_ABI_VERSION 4
+#define RGC_ABI_VERSION 5
 
 /* flags for rgc_batch_in.flags */
 #define RGC_F_GET_CC         1u  /* --get_cc   (get_cliques.py:151-156) */
@@ -180,6 +182,48 @@ int rgc_ilp_solve(rgc_ctx* ctx, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact
 
 int rgc_parse_files(const char* const* paths, int64_t n_files, int n_threads, rgc_parsed** out);
 void rgc_parsed_free(rgc_parsed* p);
+
+/* Native output writer (ABI 5), reference get_cliques.py:204-229: the pickles are emitted in
+ * the opcode layout of CPython's pickler for these objects (protocol 5, no FRAME opcodes);
+ * the names below come from the installed numpy / scipy.  repic_amd/writers.py enables it
+ * only after rgc_pickle_bytes matched pickle.dumps of the same objects. */
+typedef struct rgc_pickle_fmt {
+  const char* arr_mod;     /* numpy array reduction: module and function ("_frombuffer") */
+  const char* arr_fn;
+  const char* dtype_mod;   /* numpy.dtype class */
+  const char* dtype_cls;
+  const char* coo_mod;     /* scipy.sparse coo_matrix class */
+  const char* coo_cls;
+  int32_t maxprint;        /* coo_matrix().maxprint */
+} rgc_pickle_fmt;
+
+typedef struct rgc_write_in {
+  const char* out_dir;
+  int32_t n_mg;
+  int32_t k;
+  const char* const* bases;   /* [n_mg] output base names */
+  const int64_t* clique_off;  /* [n_mg+1] ranges into the per-clique arrays */
+  const int32_t* n_vert;      /* [n_mg] V (rows of the constraint matrix) */
+  const int32_t* cc_max;      /* [n_mg] runtime.tsv columns 2-3 */
+  const int32_t* cc_cnt;
+  const double* seconds;      /* [n_mg] runtime.tsv column 1 */
+  const float* w;             /* [C] */
+  const float* conf;          /* [C] */
+  const int32_t* rows;        /* [C*k] ascending per clique */
+  const double* cx;           /* [C] consensus x, y, global id */
+  const double* cy;
+  const int64_t* cid;
+} rgc_write_in;
+/* Writes the 5 files of every micrograph (n_threads threads); on an I/O error returns -errno
+ * and the failing micrograph in *failed_mg (the lowest of the failing ones). */
+int rgc_write_outputs(const rgc_pickle_fmt* fmt, const rgc_write_in* in, int n_threads,
+                      int64_t* failed_mg);
+/* Bytes of pickle `which` (0 weight_vector, 1 consensus_coords, 2 consensus_confidences,
+ * 3 constraint_matrix) of micrograph mg: *len always, copied when cap >= *len. */
+int rgc_pickle_bytes(const rgc_pickle_fmt* fmt, const rgc_write_in* in, int mg, int which,
+                     uint8_t* buf, int64_t cap, int64_t* len);
+/* CPython str(float) (test hook of the runtime.tsv formatting); returns the length. */
+int rgc_py_float_repr(double v, char* buf, int cap);
 
 /* Host test hooks for the CPython set-order emulation (pyset.h). */
 uint64_t rgc_py_hash_node(double x, double y, int64_t id);

@@ -124,15 +124,51 @@ __device__ __forceinline__ int wave_incl_max32(int v) {
   return v;
 }
 
+// float minimum across the wave (lane 63: the result); lanes without a source lane read +inf.
+// v_min_f32 through asm: no sNaN canonicalisation of the DPP operand (inputs are never NaN)
+__device__ __forceinline__ float vmin_f32(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float wave_incl_min_f32(float v) {
+  const int inf = 0x7f800000;
+#define RGC_DPP_MIN(ctrl, rm, bc)                                                          \
+  v = vmin_f32(v, __int_as_float(__builtin_amdgcn_update_dpp(inf, __float_as_int(v), ctrl, \
+                                                             rm, 0xf, bc)))
+  RGC_DPP_MIN(0x111, 0xf, false);
+  RGC_DPP_MIN(0x112, 0xf, false);
+  RGC_DPP_MIN(0x114, 0xf, false);
+  RGC_DPP_MIN(0x118, 0xf, false);
+  RGC_DPP_MIN(0x142, 0xa, false);
+  RGC_DPP_MIN(0x143, 0xc, false);
+#undef RGC_DPP_MIN
+  return v;
+}
+
 // In-place exclusive scan of a[0..n) in LDS whose total fits 31 bits (u16 arrays: boxes,
 // edges, vertices), a[n] = total, on 32-bit DPP wave scans; same barriers and contract as
 // block_scan_dpp below (lds: BS / 64 ints).
 template <int BS, typename A>
 __device__ __forceinline__ int block_scan_dpp32(A* a, int n, int* lds) {
-  const int per = (n + BS - 1) / BS;
+  // u16 arrays (4-byte aligned): each thread an even-length chunk read and written as u32
+  // pairs (half the LDS operations); an odd tail element only in the last chunk
+  constexpr bool PAIRS = sizeof(A) == 2;
+  const int per0 = (n + BS - 1) / BS;
+  const int per = PAIRS ? (per0 + 1) & ~1 : per0;
   const int c0 = min((int)threadIdx.x * per, n), c1 = min(c0 + per, n);
+  uint32_t* a2 = reinterpret_cast<uint32_t*>(a);
+  const int ce = PAIRS ? c0 + ((c1 - c0) & ~1) : c1;   // end of the pairs
   int s = 0;
-  for (int c = c0; c < c1; ++c) s += a[c];
+  if constexpr (PAIRS) {
+    for (int c = c0; c < ce; c += 2) {
+      const uint32_t v = a2[c >> 1];
+      s += (int)(v & 0xFFFFu) + (int)(v >> 16);
+    }
+    if (ce < c1) s += a[ce];
+  } else {
+    for (int c = c0; c < c1; ++c) s += a[c];
+  }
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int inc = wave_incl_add32(s);
   if (l == 63) lds[w] = inc;
@@ -144,10 +180,20 @@ __device__ __forceinline__ int block_scan_dpp32(A* a, int n, int* lds) {
     pre += (i < w) ? x : 0;
     tot += x;
   }
-  for (int c = c0; c < c1; ++c) {
-    const int v = a[c];
-    a[c] = (A)pre;
-    pre += v;
+  if constexpr (PAIRS) {
+    for (int c = c0; c < ce; c += 2) {
+      const uint32_t v = a2[c >> 1];
+      const int p1 = pre + (int)(v & 0xFFFFu);
+      a2[c >> 1] = ((uint32_t)pre & 0xFFFFu) | ((uint32_t)p1 << 16);
+      pre = p1 + (int)(v >> 16);
+    }
+    if (ce < c1) a[ce] = (A)pre;
+  } else {
+    for (int c = c0; c < c1; ++c) {
+      const int v = a[c];
+      a[c] = (A)pre;
+      pre += v;
+    }
   }
   if (threadIdx.x == BS - 1) a[n] = (A)tot;
   __syncthreads();

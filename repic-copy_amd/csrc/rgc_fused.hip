@@ -278,10 +278,20 @@ __device__ __forceinline__ GridU grid_u(const FusedHdr& H) {
 
 // P1 sort key of a box of picker p: its cell in picker p's grid (x-major), or nkey when the
 // box cannot have an edge (non-finite coordinates).  Monotone in x and y per picker.
+// f32 layout (!W): on floats.  The column is floor of the very product P2's half-column test
+// takes (f32 difference of the exact f32 values, times (float)inv_cell), and any consistent
+// map with the cell sizes' slack keeps the stencil exact (see P1).
+template <bool W>
 __device__ __forceinline__ int box_key(const GridU& H, int p, double x, double y) {
   if (H.ncell == 0 || !isfinite(x) || !isfinite(y)) return H.nkey;
-  const int cx = (int)fmin(floor((x - H.minx) * H.inv_cell), (double)(H.gx - 1));
-  const int cy = (int)fmin(floor((y - H.miny) * H.inv_celly), (double)(H.gy - 1));
+  int cx, cy;
+  if constexpr (W) {
+    cx = (int)fmin(floor((x - H.minx) * H.inv_cell), (double)(H.gx - 1));
+    cy = (int)fmin(floor((y - H.miny) * H.inv_celly), (double)(H.gy - 1));
+  } else {
+    cx = min((int)floorf(((float)x - (float)H.minx) * H.inv_cellf), H.gx - 1);
+    cy = min((int)floorf(((float)y - (float)H.miny) * (float)H.inv_celly), H.gy - 1);
+  }
   return p * H.ncell + cx * H.gy + cy;
 }
 
@@ -775,7 +785,7 @@ __device__ __forceinline__ void stencil_setup(Stencil& st, int ts, const FShared
   cx -= (cx * gy > cell) ? 1 : 0;
   const int cy = cell - cx * gy;
   // half-column test in f32 (0.0014 columns of slack, see P1): left half -> columns cx-1, cx
-  const float u = (float)(st.a.x - H.minx) * H.inv_cellf;
+  const float u = (float)(st.a.x - H.minx) * H.inv_cellf;   // = box_key's product on !W
   st.p = p;
   st.cx = cx - ((u - (float)cx) < 0.5f ? 1 : 0);
   st.y0 = max(cy - 1, 0);
@@ -1107,8 +1117,10 @@ void k_fused(FusedArgs A) {
   {
     BT bv[4] = {bmnx, bmny, -bmxx, -bmxy};
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      bv[r] = wave_incl_scan(bv[r], [](BT a, BT b) { return fmin(a, b); });
+    for (int r = 0; r < 4; ++r) {
+      if constexpr (W) bv[r] = wave_incl_scan(bv[r], [](BT a, BT b) { return fmin(a, b); });
+      else bv[r] = wave_incl_min_f32(bv[r]);
+    }
     if ((tid & 63) == 63)
 #pragma unroll
       for (int r = 0; r < 4; ++r) H.red4[r][tid >> 6] = (double)bv[r];
@@ -1200,7 +1212,7 @@ void k_fused(FusedArgs A) {
   // pos[i] between the passes.
   uint32_t* cw = reinterpret_cast<uint32_t*>(S.cstart);
   each_box([&](int i, double xv, double yv) {
-    const int q = box_key(G, picker_of<K>(c.pb, i), xv, yv) + 1;
+    const int q = box_key<W>(G, picker_of<K>(c.pb, i), xv, yv) + 1;
     S.pos[i] = (uint16_t)q;
     atomicAdd(&cw[q >> 1], 1u << (16 * (q & 1)));
   });
@@ -1220,6 +1232,7 @@ void k_fused(FusedArgs A) {
     const int q = S.pos[i];
     const int lo = S.cstart[q - 1], hi = S.cstart[q];
     int t = lo;
+#pragma nounroll
     for (int u = lo; u < hi; ++u) t += (int)arrival[u] < i ? 1 : 0;
     S.scell[t] = (uint16_t)(q - 1);
     S.citems[t] = (uint16_t)i;

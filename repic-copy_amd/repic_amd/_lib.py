@@ -56,6 +56,21 @@ class Parsed(C.Structure):
                 ("y", _f64p), ("score", _f64p), ("sigmoid", _u8p)]
 
 
+class PickleFmt(C.Structure):
+    _fields_ = [("arr_mod", C.c_char_p), ("arr_fn", C.c_char_p), ("dtype_mod", C.c_char_p),
+                ("dtype_cls", C.c_char_p), ("coo_mod", C.c_char_p), ("coo_cls", C.c_char_p),
+                ("maxprint", C.c_int32)]
+
+
+class WriteIn(C.Structure):
+    _fields_ = [("out_dir", C.c_char_p), ("n_mg", C.c_int32), ("k", C.c_int32),
+                ("bases", C.POINTER(C.c_char_p)), ("clique_off", C.c_void_p),
+                ("n_vert", C.c_void_p), ("cc_max", C.c_void_p), ("cc_cnt", C.c_void_p),
+                ("seconds", C.c_void_p), ("w", C.c_void_p), ("conf", C.c_void_p),
+                ("rows", C.c_void_p), ("cx", C.c_void_p), ("cy", C.c_void_p),
+                ("cid", C.c_void_p)]
+
+
 lib.rgc_abi_version.restype = C.c_int
 lib.rgc_last_error.restype = C.c_char_p
 lib.rgc_device_count.argtypes = [C.POINTER(C.c_int)]
@@ -80,10 +95,17 @@ lib.rgc_test_epilogue.argtypes = [C.c_int, _f64p, _f64p, _f64p, C.POINTER(C.c_in
                                   C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_int),
                                   C.POINTER(C.c_int8), _f32p, _f32p]
 
+lib.rgc_write_outputs.argtypes = [C.POINTER(PickleFmt), C.POINTER(WriteIn), C.c_int,
+                                  C.POINTER(C.c_int64)]
+lib.rgc_pickle_bytes.argtypes = [C.POINTER(PickleFmt), C.POINTER(WriteIn), C.c_int, C.c_int,
+                                 C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
+lib.rgc_py_float_repr.argtypes = [C.c_double, C.c_char_p, C.c_int]
+
 EXPORTS = ["rgc_abi_version", "rgc_last_error", "rgc_device_count", "rgc_ctx_create",
            "rgc_ctx_destroy", "rgc_run", "rgc_submit", "rgc_wait", "rgc_kernel_times", "rgc_last_edges", "rgc_parse_files",
            "rgc_parsed_free", "rgc_py_hash_node", "rgc_py_set_order", "rgc_test_epilogue",
-           "rgc_score_pairs", "rgc_ilp_solve"]
+           "rgc_score_pairs", "rgc_ilp_solve", "rgc_write_outputs", "rgc_pickle_bytes",
+           "rgc_py_float_repr"]
 
 
 class RGCError(RuntimeError):
