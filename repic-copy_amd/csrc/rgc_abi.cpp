@@ -60,6 +60,8 @@ enum DevBufId {
   D_BPICK, D_FWDCNT, D_FWDOFF, D_TILES, D_TOTAL, D_EDST, D_EJI, D_PARENT, D_HASEDGE, D_CSIZE,
   D_STAT, D_INSKEY, D_COMPMIN, D_CCOUNT, D_COFF, D_INCL, D_VLIST, D_VSORT, D_VROW, D_BOFF, D_RLO, D_ADJG, D_RBOUND, D_RFLAG, D_DFSMG, D_ROOTBOX, D_EXLIST,
   D_LCNT, D_LOFF, D_LROOT0, D_LROOT1, D_LM0, D_LM1, D_LP0, D_LP1, D_PK,
+  // HBM level-tree slots of the 1024-thread fused launches (K >= 4)
+  D_QG, D_QGSLOT,
   // RGC_F_EDGES test hook
   D_EU, D_EV, D_EJIOUT,
   // score_detections raster
@@ -209,6 +211,7 @@ struct rgc_ctx {
   rgc_batch_in pin{};      // the submitted batch (caller keeps its arrays alive until rgc_wait)
   rgc_batch_out pend_out{};
   hipEvent_t ev_sub = nullptr;   // after the submitted run's stats copy
+  int qg_nslots = 0;             // HBM level-tree slots allocated (ensure_qg)
 };
 
 static int ensure_dev(rgc_ctx* c, int id, size_t bytes, size_t keep = 0) {
@@ -226,6 +229,32 @@ static int ensure_dev(rgc_ctx* c, int id, size_t bytes, size_t keep = 0) {
   if (b.p) HIPCHK(hipFree(b.p));
   b.p = p;
   b.cap = cap;
+  return 0;
+}
+
+// HBM level-tree slots of the 1024-thread fused launches (K = 4, rgc_fused.hip P4): twice as
+// many as the CUs (LDS admits one such workgroup per CU), QG_BYTES each; the slot bitmap is
+// zeroed once and every workgroup clears its bit again before it ends.
+constexpr int QG_BYTES = 1 << 20;
+static int ensure_qg(rgc_ctx* c, FusedArgs& A, int k, int nt) {
+  A.qg_base = nullptr;
+  A.qg_slots = nullptr;
+  A.qg_nslots = 0;
+  A.qg_bytes = 0;
+  if (nt != 1024 || k != 4) return 0;
+  if (!c->qg_nslots) {
+    int ncu = 0;
+    HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
+    const int ns = (2 * std::max(ncu, 1) + 31) / 32 * 32;
+    TRY(ensure_dev(c, D_QG, (size_t)ns * QG_BYTES));
+    TRY(ensure_dev(c, D_QGSLOT, (size_t)ns / 8));
+    HIPCHK(hipMemsetAsync(c->d[D_QGSLOT].p, 0, (size_t)ns / 8, c->stream));
+    c->qg_nslots = ns;
+  }
+  A.qg_base = static_cast<char*>(c->d[D_QG].p);
+  A.qg_slots = static_cast<uint32_t*>(c->d[D_QGSLOT].p);
+  A.qg_nslots = c->qg_nslots;
+  A.qg_bytes = QG_BYTES;
   return 0;
 }
 
@@ -767,6 +796,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
 #ifdef RGC_STAMPS
           A.stamps = D<unsigned long long>(c, D_STAMPS) + (size_t)(ml_off + starts[q]) * 16;
 #endif
+          TRY(ensure_qg(c, A, k, pl.nt));
           TRY(mark(c, "k_fused"));
           const int le = launch_fused(s, single ? n_mg : (int)lists[q].size(), pl.lds, A, wide,
                                       pl.nt);
@@ -1030,6 +1060,7 @@ static int submit_fast(rgc_ctx* c, const rgc_batch_in* in) {
 #ifdef RGC_STAMPS
   return 0;   // the diagnostic build times through rgc_run only
 #endif
+  TRY(ensure_qg(c, A, k, pl.nt));
   TRY(mark(c, "k_fused"));
   const int le = launch_fused(s, n_mg, pl.lds, A, false, pl.nt);
   if (le != 0) return fail("fused kernel launch failed (submit): " +

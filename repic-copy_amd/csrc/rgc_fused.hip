@@ -56,6 +56,7 @@ struct FusedHdr {
   int E, nodes, cc_cnt, cc_max, target, V, status;
   uint32_t ccur;    // P4 clique-queue cursor
   int tief[2];      // P6: some clique of the chunk needs the order pass (by chunk parity)
+  int qslot;        // QG: the workgroup's HBM level-tree slot (-1: none, LDS queue)
   int64_t C, base;
 };
 
@@ -996,7 +997,29 @@ constexpr int fused_waves_per_eu(int k, int nt) {
 }
 #endif
 
-template <int K, bool W, int NT>
+// HBM level-tree slots (QG launches): claim a free bit of the slot bitmap (one thread), or -1
+// after a bounded search (then the workgroup keeps the LDS queue).  There are twice as many
+// slots as workgroups of such a launch can be resident, so the search normally succeeds on
+// its first pass; every claimed slot is released by its workgroup before it ends.
+__device__ int qg_claim(const FusedArgs& A) {
+  const int nw = A.qg_nslots >> 5;
+  const int w0 = (int)(blockIdx.x % (unsigned)max(nw, 1));
+  for (int pass = 0; pass < 4; ++pass) {
+    for (int i = 0; i < nw; ++i) {
+      const int wd = (w0 + i) % nw;
+      uint32_t v = __hip_atomic_load(A.qg_slots + wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int t = 0; t < 32 && v != 0xFFFFFFFFu; ++t) {
+        const int b = __builtin_ctz(~v);
+        const uint32_t old = atomicOr(A.qg_slots + wd, 1u << b);
+        if (!(old & (1u << b))) return wd * 32 + b;
+        v = old | (1u << b);
+      }
+    }
+  }
+  return -1;
+}
+
+template <int K, bool W, int NT, bool QG>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(fused_waves_per_eu(K, NT))))
 void k_fused(FusedArgs A) {
   constexpr int FWG = NT;   // threads of this instance
@@ -1457,8 +1480,21 @@ void k_fused(FusedArgs A) {
   // queue region: after the E used entries of dst through the cell starts (contiguous: dst
   // immediately precedes the cell starts in the layout)
   const int qoff = (L.off_dst + 2 * H.E + 15) & ~15;
-  const int qbytes = L.off_parent - qoff;
-  char* const q = smem + qoff;
+  const int qbytes_lds = L.off_parent - qoff;
+  char* q = smem + qoff;
+  int qbytes = qbytes_lds;
+  int qslot = -1;
+  if constexpr (QG) {
+    // large micrographs: the level trees in an HBM slot (no root chunks to re-walk), the
+    // LDS region when no slot is free
+    if (tid == 0) H.qslot = A.qg_base ? qg_claim(A) : -1;
+    __syncthreads();
+    qslot = ufl(H.qslot);
+    if (qslot >= 0) {
+      q = A.qg_base + (size_t)qslot * (size_t)A.qg_bytes;
+      qbytes = A.qg_bytes;
+    }
+  }
   // Root chunks: all roots at once when the levels fit the queue region, else consecutive
   // root ranges (halved after a level overflows, doubled after a success).  Chunk i covers
   // roots [rs[i], rs[i+1]) and cliques [cs[i], cs[i+1]) of the micrograph's lexicographic
@@ -1502,7 +1538,7 @@ void k_fused(FusedArgs A) {
     c.cq_cap = (int)max(bo.C, (int64_t)1);
     c.cq_ord = reinterpret_cast<uint16_t*>(q + bo.lvl[K] + 4 * (int)bo.C);
   } else {
-    S.cbuf = reinterpret_cast<uint16_t*>(smem + qoff);
+    S.cbuf = reinterpret_cast<uint16_t*>(smem + qoff);   // (LDS even when QG)
     c.cq_cap = 0;   // the DFS only counts; P6 re-walks it chunk by chunk
     c.ccur = &H.ccur;
     for (int r = tid; r < n0; r += FWG) {
@@ -1519,7 +1555,7 @@ void k_fused(FusedArgs A) {
     __syncthreads();
     C = block_scan_dpp<FWG>(S.cnt, n0, H.red64);
     if (tid == 0) S.cnt[n0] = (uint32_t)C;
-    c.cq_cap = qbytes / (2 * K + 2);
+    c.cq_cap = qbytes_lds / (2 * K + 2);
     c.cq_ord = S.cbuf + (size_t)c.cq_cap * K;
   }
   c.S.cbuf = S.cbuf;
@@ -1694,24 +1730,33 @@ void k_fused(FusedArgs A) {
     }
   }
   STAMP(12);
+  if constexpr (QG) {
+    if (qslot >= 0) {   // every thread is done with the slot
+      __syncthreads();
+      if (tid == 0) {
+        __threadfence();
+        atomicAnd(A.qg_slots + (qslot >> 5), ~(1u << (qslot & 31)));
+      }
+    }
+  }
   if (tid == 0)
     put_stats(A, m, H.status, H.E, H.nodes, H.cc_cnt, H.cc_max, H.V, H.base, H.C);
 }
 
-template <int K, bool W, int NT>
+template <int K, bool W, int NT, bool QG = false>
 static int launch_fused_t(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArgs& A) {
   static std::atomic<uint64_t> attr_set{0};   // per device
-  const hipError_t e = set_dyn_lds_once(attr_set, reinterpret_cast<const void*>(&k_fused<K, W, NT>),
+  const hipError_t e = set_dyn_lds_once(attr_set, reinterpret_cast<const void*>(&k_fused<K, W, NT, QG>),
                                         160 * 1024);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL((k_fused<K, W, NT>), dim3(n_blocks), dim3(NT), lds_bytes, stream, A);
+  hipLaunchKernelGGL((k_fused<K, W, NT, QG>), dim3(n_blocks), dim3(NT), lds_bytes, stream, A);
   return (int)hipGetLastError();
 }
 
-template <int K, bool W, int NT>
+template <int K, bool W, int NT, bool QG = false>
 static int fused_vgprs_t() {
   hipFuncAttributes at;
-  if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&k_fused<K, W, NT>)) != hipSuccess)
+  if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&k_fused<K, W, NT, QG>)) != hipSuccess)
     return -1;
   return at.numRegs;
 }
@@ -1729,7 +1774,7 @@ static int fused_vgprs_k(int nt) {
   }
   if constexpr (K <= 5) {
     if (nt == 768) return fused_vgprs_t<K, W, 768>();
-    if (nt == 1024) return fused_vgprs_t<K, W, 1024>();
+    if (nt == 1024) return fused_vgprs_t<K, W, 1024, (K == 4)>();
   }
   return nt == 512 ? fused_vgprs_t<K, W, 512>() : -1;
 }
@@ -1742,7 +1787,9 @@ static int launch_fused_k(hipStream_t stream, int n_blocks, int lds_bytes, const
   }
   if constexpr (K <= 5) {
     if (nt == 768) return launch_fused_t<K, W, 768>(stream, n_blocks, lds_bytes, A);
-    if (nt == 1024) return launch_fused_t<K, W, 1024>(stream, n_blocks, lds_bytes, A);
+    // 1024 threads (LDS admits one workgroup per CU): K = 4 level trees in HBM slots (K = 5
+    // keeps the LDS queue: the flat pointers would push it past 128 VGPRs into scratch)
+    if (nt == 1024) return launch_fused_t<K, W, 1024, (K == 4)>(stream, n_blocks, lds_bytes, A);
   }
   return nt == 512 ? launch_fused_t<K, W, 512>(stream, n_blocks, lds_bytes, A) : -1;
 }

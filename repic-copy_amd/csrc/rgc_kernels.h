@@ -108,6 +108,11 @@ struct FusedArgs {
   int32_t* ev;
   double* eji;
   int64_t ecap_out;
+  // level trees of the 1024-thread launches (K = 4) in HBM: qg_nslots slots of qg_bytes,
+  // claimed per workgroup through the qg_slots bitmap (nullptr: LDS queue only)
+  char* qg_base;
+  uint32_t* qg_slots;
+  int qg_nslots, qg_bytes;
 };
 
 int fused_lds_bytes(int nmax, int ecap, bool wide);
