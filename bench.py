@@ -425,10 +425,11 @@ def main():
     dev_ms = sum(v for k_, v in avg.items() if k_ not in ("d2h", "h2d_meta", "d2h_stats"))
     pipe = pipeline_bytes(N, E, C, cfg.k)
     if avg.get("k_fused", 0.0) >= 0.5 * dev_ms:
-        # fused route: one kernel runs the whole hot path, its B_alg is the pipeline's
+        # fused route: one kernel runs the whole hot path (plus k_fused_ties, the CPython
+        # set-order tie-breaks it hands off), its B_alg is the pipeline's
         dom = "k_fused"
         dom_bytes = alg_bytes(dom, N, E, C, cfg.k, V, n_mg)
-        dom_ms = avg[dom]
+        dom_ms = avg[dom] + avg.get("k_fused_ties", 0.0)
     else:
         # large-micrograph route (C3, C5): SURVEY.md §8(d) prices the whole route,
         # achieved = sum B_alg / device time of all its kernels (rocprof: their sum)
@@ -463,7 +464,9 @@ def main():
                      "alg_bytes_per_step": dom_bytes, "alg_bytes_formula":
                          "SURVEY.md 8(d): 28 N + 32 E + C (20 k + 12)",
                      "compulsory_bytes_per_step": fused_compulsory_bytes(N, C, cfg.k, V, n_mg),
-                     "kernel_ms_per_step": dom_ms},
+                     "kernel_ms_per_step": dom_ms,
+                     "kernel_ms_parts": {k_: round(avg[k_], 5) for k_ in ("k_fused", "k_fused_ties")
+                                         if k_ in avg} if dom == "k_fused" else None},
         "pipeline": {"device_ms_per_step": dev_ms, "alg_bytes": pipe,
                      "achieved_gbs": pipe / (dev_ms * 1e-3) / 1e9,
                      "frac": pipe / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,

@@ -36,6 +36,14 @@ PYS_FN uint64_t hash_double(double v) {
     if (isinf(v)) return v > 0 ? HASH_INF : (uint64_t)(-(int64_t)HASH_INF);
     return 0;  // unreachable for graph nodes (NaN coordinates never form edges)
   }
+  // integral values below 2^53 (integer pixel coordinates): CPython guarantees
+  // hash(x) == hash(int(x)), i.e. sign * (|x| mod P) with |x| < P, -1 -> -2; this skips the
+  // frexp / 28-bit mantissa loop for them (same result as the loop below)
+  if (fabs(v) < 9007199254740992.0 && v == trunc(v)) {
+    uint64_t x = (uint64_t)(int64_t)v;
+    if (x == (uint64_t)-1) x = (uint64_t)-2;
+    return x;
+  }
   int e;
   double m = frexp(v, &e);
   int sign = 1;
@@ -59,7 +67,7 @@ PYS_FN uint64_t hash_double(double v) {
 
 // long_hash for a non-negative id.
 PYS_FN uint64_t hash_id(int64_t v) {
-  uint64_t x = (uint64_t)v % HASH_MOD;
+  uint64_t x = (uint64_t)v < HASH_MOD ? (uint64_t)v : (uint64_t)v % HASH_MOD;
   if (x == (uint64_t)-1) x = (uint64_t)-2;
   return x;
 }

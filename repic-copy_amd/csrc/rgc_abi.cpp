@@ -62,6 +62,8 @@ enum DevBufId {
   D_LCNT, D_LOFF, D_LROOT0, D_LROOT1, D_LM0, D_LM1, D_LP0, D_LP1, D_PK,
   // HBM level-tree slots of the 1024-thread fused launches (K >= 4)
   D_QG, D_QGSLOT,
+  // set-order tie entries of the fused launches (k_fused_ties)
+  D_TIES,
   // RGC_F_EDGES test hook
   D_EU, D_EV, D_EJIOUT,
   // score_detections raster
@@ -111,8 +113,9 @@ struct FusedPlan {
 // Workgroups per CU the VGPRs of the nt-thread kernel allow (nt / 64 waves per workgroup over
 // 4 SIMDs of 512 VGPRs, at most 8 waves per SIMD).
 static int vgpr_wg_cap(int k, bool wide, int nt) {
-  static int cache[2][MAX_K + 1][4] = {};
-  int& v = cache[wide][k][std::min(3, std::max(0, nt / 256 - 1))];
+  static int cache[2][MAX_K + 1][5] = {};
+  const int slot = nt == 256 ? 0 : nt == 384 ? 1 : nt == 512 ? 2 : nt == 768 ? 3 : 4;
+  int& v = cache[wide][k][slot];
   if (!v) {
     const int r = fused_vgprs(k, wide, nt);
     const int waves = r > 0 ? std::min(8, 512 / (((r + 7) / 8) * 8)) : 0;
@@ -136,7 +139,7 @@ static bool plan_fused(int k, bool wide, int nmax, int max_wg, FusedPlan* p) {
     return e ? atoi(e) : 0;
   }();
   int w = 0, nt = 512, best_waves = 0;
-  for (int cand : {256, 512, 768, 1024}) {
+  for (int cand : {256, 384, 512, 768, 1024}) {
     if (!fused_nt_ok(k, cand) || (diag_nt && fused_nt_ok(k, diag_nt) && cand != diag_nt)) continue;
     const int wc = std::min(std::min(max_wg, vgpr_wg_cap(k, wide, cand)), LDS_BLOCKS / need);
     if (wc < 1) continue;
@@ -297,6 +300,7 @@ static int ensure_outputs(rgc_ctx* c, int64_t need, int64_t keep, int k, bool me
   TRY(ensure_dev(c, D_W, need * 4, keep * 4));
   TRY(ensure_dev(c, D_CONF, need * 4, keep * 4));
   TRY(ensure_dev(c, D_CONS, need * 4, keep * 4));
+  TRY(ensure_dev(c, D_TIES, need * (4 + k) * 4));   // <= one entry per clique
   if (members) TRY(ensure_dev(c, D_MEMBERS, need * k * 4, keep * k * 4));
   if (multi) TRY(ensure_dev(c, D_ORDER, need * k, keep * k));
   return 0;
@@ -744,6 +748,9 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
       A.ev = want_edges ? D<int32_t>(c, D_EV) : nullptr;
       A.eji = want_edges ? D<double>(c, D_EJIOUT) : nullptr;
       A.ecap_out = c->cap_edges;
+      A.tie_list = D<int32_t>(c, D_TIES);
+      A.tie_cap = c->cap_cliques;
+      int64_t ties_done = 0;   // entries of earlier passes already resolved
 #ifdef RGC_STAMPS
       TRY(ensure_dev(c, D_STAMPS, 3 * (size_t)n_mg * 16 * 8));
       HIPCHK(hipMemsetAsync(D<void>(c, D_STAMPS), 0, 3 * (size_t)n_mg * 128, s));
@@ -807,6 +814,8 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
                         std::to_string(pl.nt) + " threads): " +
                         (le > 0 ? hipGetErrorString((hipError_t)le) : "unsupported k"));
         }
+        TRY(mark(c, "k_fused_ties"));
+        if (launch_fused_ties(s, A, ties_done) != 0) return fail("tie kernel launch failed");
         TRY(mark(c, "d2h_stats"));
         HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOUT), D<void>(c, D_MGOUT), cur_off + 2 * CUR_BYTES,
                               hipMemcpyDeviceToHost, s));
@@ -817,6 +826,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
         HIPCHK(hipGetLastError());
         HIPCHK(hipStreamSynchronize(s));
         const int32_t* fst = ho.status;
+        ties_done = std::min<int64_t>((int64_t)h_cur[3], A.tie_cap);
         ml_off += (int)by.size();
         todo.clear();
         auto check = [&](int32_t m) {
@@ -1057,6 +1067,8 @@ static int submit_fast(rgc_ctx* c, const rgc_batch_in* in) {
   A.stamps = nullptr;
   A.eu = nullptr; A.ev = nullptr; A.eji = nullptr; A.ecap_out = 0;
   A.nmax = pl.nmax; A.ecap = pl.ecap; A.mg_list = nullptr;
+  A.tie_list = D<int32_t>(c, D_TIES);
+  A.tie_cap = c->cap_cliques;
 #ifdef RGC_STAMPS
   return 0;   // the diagnostic build times through rgc_run only
 #endif
@@ -1065,6 +1077,8 @@ static int submit_fast(rgc_ctx* c, const rgc_batch_in* in) {
   const int le = launch_fused(s, n_mg, pl.lds, A, false, pl.nt);
   if (le != 0) return fail("fused kernel launch failed (submit): " +
                            std::string(le > 0 ? hipGetErrorString((hipError_t)le) : "unsupported k"));
+  TRY(mark(c, "k_fused_ties"));
+  if (launch_fused_ties(s, A, 0) != 0) return fail("tie kernel launch failed (submit)");
   c->pend_slot = io.slot;
   c->cur_slot = 1 - c->cur_slot;   // the launch zeroes the other slot: the next run's
   if (c->timing) {

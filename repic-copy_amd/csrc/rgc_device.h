@@ -422,6 +422,21 @@ struct Epi {
   int8_t ord[K];  // networkx node-iteration order (picker indices)
 };
 
+// graph insertion order of a clique's members by their insertion keys (nibble r = member
+// index of the r-th node; ties by member index)
+template <int K>
+__host__ __device__ __forceinline__ uint32_t node_order_ins(const uint64_t (&ins)[K]) {
+  uint32_t ord = 0;
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    int rk = 0;
+#pragma unroll
+    for (int q = 0; q < K; ++q) rk += (ins[q] < ins[i] || (ins[q] == ins[i] && q < i)) ? 1 : 0;
+    ord |= (uint32_t)i << (4 * rk);
+  }
+  return ord;
+}
+
 // networkx node-iteration order of a clique (nibble r = member index of the r-th node): set
 // order = CPython set(sorted(clique)) iteration (2k < |G|), else graph insertion order.
 // Needed only on weighted-degree ties or for --multi_out.
@@ -470,13 +485,7 @@ __host__ __device__ __forceinline__ uint32_t node_order(const int (&mem)[K], con
       ord |= ((inv >> (4 * t)) & 15) << (4 * r);
     }
   } else {
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-      int rk = 0;
-#pragma unroll
-      for (int q = 0; q < K; ++q) rk += (ins[q] < ins[i] || (ins[q] == ins[i] && q < i)) ? 1 : 0;
-      ord |= (uint32_t)i << (4 * rk);
-    }
+    ord = node_order_ins<K>(ins);
   }
   return ord;
 }

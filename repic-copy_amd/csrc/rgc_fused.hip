@@ -155,6 +155,9 @@ struct FCtx {
   uint16_t* cq_ord;  // P4 queue: ordinal of each queued clique within its root's DFS
   uint32_t* ccur;    // P4 queue cursor (LDS)
   int cq_cap;        // P4 queue capacity (cliques)
+  int32_t* tie_list;              // set-order ties for k_fused_ties
+  unsigned long long* tie_count;
+  int64_t tie_cap;
 };
 
 __device__ __forceinline__ uint32_t lds_ld(uint32_t* p) {
@@ -394,7 +397,11 @@ __device__ __forceinline__ bool fused_epilogue_main(const FCtx<K>& c, int64_t j,
       mid_n<NE>(Is);
       if (NE & 1) {
         med = (double)Is[NE / 2];
+#ifdef RGC_X_NODIV   // timing experiment only
+        med = med * c.two_b2;
+#else
         med = med / (c.two_b2 - med);
+#endif
       } else {
         const double a = (double)Is[NE / 2 - 1], b = (double)Is[NE / 2];
         med = ((a / (c.two_b2 - a)) + (b / (c.two_b2 - b))) / 2.0;
@@ -464,7 +471,6 @@ __device__ __forceinline__ void fused_epilogue_order(const FCtx<K>& c, int64_t j
                                                      const int (&mem)[K]) {
   double ji[K][K], xs[K], ys[K];
   int li[K];
-  int64_t ids[K];
   uint64_t ins[K] = {};
 #pragma unroll
   for (int i = 0; i < K; ++i) {
@@ -472,7 +478,6 @@ __device__ __forceinline__ void fused_epilogue_order(const FCtx<K>& c, int64_t j
     xs[i] = xy.x;
     ys[i] = xy.y;
     li[i] = c.S.citems[mem[i]];
-    ids[i] = c.idb + li[i];
   }
 #pragma unroll
   for (int a = 0; a < K; ++a)
@@ -484,12 +489,29 @@ __device__ __forceinline__ void fused_epilogue_order(const FCtx<K>& c, int64_t j
   uint32_t top;
   int arg = epi_degree_max<K>(ji, &top);
   const bool tie = (top & (top - 1)) != 0;
-  if (tie || (c.flags & 2)) {
-    const uint32_t ord = node_order<K>(li, xs, ys, ids, c.set_order, ins);
-    if (tie) arg = epi_tie_arg<K>(top, ord);
-    if (c.flags & 2) {
+  const bool multi = (c.flags & 2) != 0;
+  if (tie || multi) {
+    if (c.set_order) {
+      // CPython set order (64-bit tuple hashing and set probing): appended for k_fused_ties,
+      // which keeps that code out of this kernel's registers (ties: ~0.6 % of C2's cliques)
+      const unsigned long long t = atomicAdd(c.tie_count, 1ull);
+      if ((int64_t)t < c.tie_cap) {
+        int32_t* e = c.tie_list + (int64_t)t * (4 + K);
+        e[0] = (int32_t)(uint32_t)(uint64_t)j;
+        e[1] = (int32_t)(uint32_t)((uint64_t)j >> 32);
+        e[2] = c.m;
+        e[3] = (int32_t)(top | (tie ? 0x10000u : 0u) | (multi ? 0x20000u : 0u));
 #pragma unroll
-      for (int i = 0; i < K; ++i) c.order[j * K + i] = (uint8_t)((ord >> (4 * i)) & 15);
+        for (int i = 0; i < K; ++i) e[4 + i] = c.b0 + li[i];
+      }
+      if (tie) return;   // consensus by k_fused_ties
+    } else {
+      const uint32_t ord = node_order_ins<K>(ins);
+      if (tie) arg = epi_tie_arg<K>(top, ord);
+      if (multi) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) c.order[j * K + i] = (uint8_t)((ord >> (4 * i)) & 15);
+      }
     }
   }
   int cons = li[0];
@@ -993,7 +1015,7 @@ __device__ __forceinline__ void put_stats(const FusedArgs& A, int m, int status,
 constexpr int fused_waves_per_eu(int, int) { return 1; }
 #else
 constexpr int fused_waves_per_eu(int k, int nt) {
-  return nt == 1024 ? 4 : (nt == 768 ? 6 : (nt == 256 ? 4 : (k <= 3 ? 8 : 1)));
+  return nt == 1024 ? 4 : (nt == 768 ? 6 : (nt == 256 ? 4 : (nt == 384 ? 6 : (k <= 3 ? 8 : 1))));
 }
 #endif
 
@@ -1079,6 +1101,7 @@ void k_fused(FusedArgs A) {
   c.two_b2f = uff((float)A.two_b2);
   c.rows = A.rows; c.w = A.w; c.conf = A.conf; c.consensus = A.consensus;
   c.members = A.members; c.order = A.order;
+  c.tie_list = A.tie_list; c.tie_count = A.cursor + 3; c.tie_cap = A.tie_cap;
   c.S = S;
   c.m = m;
   c.b0 = A.box_off[m * K];
@@ -1329,7 +1352,11 @@ void k_fused(FusedArgs A) {
     // fill each list (already sorted: position order) and record each edge's source in dst's
     // unused tail when it has room; then union the edges one thread per edge (lock-free
     // union-find, balanced across lanes whatever the degrees).  Without room: union per box.
+#ifdef RGC_X_BOXUNION   // experiment: union per box inside the fill
+    const bool src_ok = false;
+#else
     const bool src_ok = 2 * E <= A.ecap;
+#endif
     uint16_t* esrc = S.dst + E;
     for (int r0 = 0, odd = 0; r0 < n; r0 += FWG, odd ^= 1) {   // same order as the count
       const int ts = odd ? r0 + FWG - 1 - tid : r0 + tid;
@@ -1364,7 +1391,9 @@ void k_fused(FusedArgs A) {
       for (int e = tid; e < E; e += FWG) {
         const uint32_t h = S.dst[e];
         S.flags[h] = 1;
+#ifndef RGC_X_NOUNION   // timing experiment only: no unions (CC stats wrong)
         uf_union_lds(S.parent, esrc[e], h);
+#endif
       }
       __syncthreads();
     }
@@ -1707,6 +1736,10 @@ void k_fused(FusedArgs A) {
       for (int sl = tid; sl < c1 - c0; sl += FWG) {
         int mem[K];
         clique_members(sl, mem);
+#ifdef RGC_X_NOEPI   // timing experiment only: members walked, no epilogue
+        if (mem[0] == 0xFFFFF) c.cq_ord[sl] = 1;
+        continue;
+#endif
         bool order;
         if (!W && c.intp) order = fused_epilogue_main<K, W, true>(c, obase + (c0 + sl), mem);
         else order = fused_epilogue_main<K, W, false>(c, obase + (c0 + sl), mem);
@@ -1717,7 +1750,11 @@ void k_fused(FusedArgs A) {
       }
       if (any) H.tief[ci & 1] = 1;
       __syncthreads();
+#ifdef RGC_X_NOORDER   // timing experiment only: no order pass (tie consensus wrong)
+      if (false) {
+#else
       if (H.tief[ci & 1]) {
+#endif
         for (int sl = tid; sl < c1 - c0; sl += FWG) {
           const uint32_t o = c.cq_ord[sl];
           if (!(o & 0x8000)) continue;
@@ -1743,6 +1780,56 @@ void k_fused(FusedArgs A) {
     put_stats(A, m, H.status, H.E, H.nodes, H.cc_cnt, H.cc_max, H.V, H.base, H.C);
 }
 
+// Consensus on set-order ties and the --multi_out node order of the cliques the fused kernel
+// appended (fused_epilogue_order): networkx iterates set(sorted(clique)) (get_cliques.py:182-183
+// -> CPython set order of the (x, y, id) node keys, pyset.h), first tied member in that order.
+// Grid-stride over the entries [from, cursor[3]).
+template <int K>
+__global__ __launch_bounds__(256) void k_fused_ties(FusedArgs A, int64_t from) {
+  const int64_t n = min((int64_t)__hip_atomic_load(A.cursor + 3, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT), A.tie_cap);
+  for (int64_t t = from + (int64_t)blockIdx.x * 256 + threadIdx.x; t < n;
+       t += (int64_t)gridDim.x * 256) {
+    const int32_t* e = A.tie_list + t * (4 + K);
+    const int64_t j = (int64_t)(((uint64_t)(uint32_t)e[1] << 32) | (uint32_t)e[0]);
+    const int m = e[2];
+    const uint32_t fl = (uint32_t)e[3];
+    const int64_t idb = A.id_base[m] - (int64_t)A.box_off[m * K];
+    int mem[K];
+    double xs[K], ys[K];
+    int64_t ids[K];
+    const uint64_t ins[K] = {};
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      mem[i] = e[4 + i];
+      xs[i] = A.x[mem[i]];
+      ys[i] = A.y[mem[i]];
+      ids[i] = idb + mem[i];
+    }
+    const uint32_t ord = node_order<K>(mem, xs, ys, ids, true, ins);
+    if (fl & 0x10000u) A.consensus[j] = mem[epi_tie_arg<K>(fl & 0xFFFFu, ord)];
+    if (fl & 0x20000u) {
+#pragma unroll
+      for (int i = 0; i < K; ++i) A.order[j * K + i] = (uint8_t)((ord >> (4 * i)) & 15);
+    }
+  }
+}
+
+int launch_fused_ties(hipStream_t stream, const FusedArgs& A, int64_t from) {
+  if (!A.tie_list || A.tie_cap <= from) return 0;
+  const dim3 g(256), b(256);
+  switch (A.k) {
+#define RGC_TIES_CASE(KK) \
+  case KK: hipLaunchKernelGGL((k_fused_ties<KK>), g, b, 0, stream, A, from); break;
+    RGC_TIES_CASE(2) RGC_TIES_CASE(3) RGC_TIES_CASE(4) RGC_TIES_CASE(5) RGC_TIES_CASE(6)
+    RGC_TIES_CASE(7) RGC_TIES_CASE(8)
+#undef RGC_TIES_CASE
+    default:
+      return -1;
+  }
+  return (int)hipGetLastError();
+}
+
 template <int K, bool W, int NT, bool QG = false>
 static int launch_fused_t(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArgs& A) {
   static std::atomic<uint64_t> attr_set{0};   // per device
@@ -1764,13 +1851,15 @@ static int fused_vgprs_t() {
 // workgroup sizes compiled for k (fused_nt_ok) and their dispatch
 bool fused_nt_ok(int k, int nt) {
   if (k < 2 || k > 8) return false;
-  return nt == 512 || ((nt == 768 || nt == 1024) && k <= 5) || (nt == 256 && k <= 3);
+  return nt == 512 || ((nt == 768 || nt == 1024) && k <= 5) ||
+         ((nt == 256 || nt == 384) && k <= 3);
 }
 
 template <int K, bool W>
 static int fused_vgprs_k(int nt) {
   if constexpr (K <= 3) {
     if (nt == 256) return fused_vgprs_t<K, W, 256>();
+    if (nt == 384) return fused_vgprs_t<K, W, 384>();
   }
   if constexpr (K <= 5) {
     if (nt == 768) return fused_vgprs_t<K, W, 768>();
@@ -1784,6 +1873,7 @@ static int launch_fused_k(hipStream_t stream, int n_blocks, int lds_bytes, const
                           int nt) {
   if constexpr (K <= 3) {
     if (nt == 256) return launch_fused_t<K, W, 256>(stream, n_blocks, lds_bytes, A);
+    if (nt == 384) return launch_fused_t<K, W, 384>(stream, n_blocks, lds_bytes, A);
   }
   if constexpr (K <= 5) {
     if (nt == 768) return launch_fused_t<K, W, 768>(stream, n_blocks, lds_bytes, A);

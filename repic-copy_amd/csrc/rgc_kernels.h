@@ -113,6 +113,11 @@ struct FusedArgs {
   char* qg_base;
   uint32_t* qg_slots;
   int qg_nslots, qg_bytes;
+  // cliques whose consensus / --multi_out order needs CPython set order (degree ties with
+  // 2k < |G|): entries of 4 + k int32 (j lo, j hi, micrograph, top | tie << 16 | multi << 17,
+  // k batch box indices) for k_fused_ties, counted on cursor[3]; tie_cap entries
+  int32_t* tie_list;
+  int64_t tie_cap;
 };
 
 int fused_lds_bytes(int nmax, int ecap, bool wide);
@@ -120,6 +125,8 @@ int fused_vgprs(int k, bool wide, int nt);
 bool fused_nt_ok(int k, int nt);
 int launch_fused(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArgs& A, bool wide,
                  int nt);
+// the tie entries [from, cursor[3]) of the fused launches before it (CPython set order)
+int launch_fused_ties(hipStream_t stream, const FusedArgs& A, int64_t from);
 void launch_gather(hipStream_t stream, int n_sub, int k, const int32_t* sub_mg,
                    const int32_t* box_off, const int32_t* sub_box_off, const double* x,
                    const double* y, const double* s, double* ox, double* oy, double* os,

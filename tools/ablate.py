@@ -48,7 +48,7 @@ class Runner:
         ms = (C.c_float * n)()
         nm = (C.c_char_p * n)()
         self.lib.rgc_kernel_times(self.ctx, n, ms, nm)
-        return sum(ms[i] for i in range(n) if nm[i] == b"k_fused")
+        return sum(ms[i] for i in range(n) if nm[i] in (b"k_fused", b"k_fused_ties"))
 
 
 runners = [Runner(p) for p in libs]
