@@ -48,7 +48,6 @@ struct FusedHdr {
     };
     double red4[4][MAXW];
   };
-  int nonint[MAXW];   // P0: per wave, some finite coordinate is not an integer in (-2^23, 2^23)
   double minx, miny, cell, inv_cell, inv_celly;
   double xbs;       // P5 x-bucket scale: bucket(x) = min(trunc((x - minx) * xbs), n - 1)
   float inv_gy;
@@ -148,7 +147,6 @@ struct FCtx {
   int m, b0, n;
   int64_t idb;       // global id of local box 0
   bool set_order;    // networkx iterates set(sorted(clique)) (2k < |G|)
-  bool intp;         // integer coordinates (P2) and B <= 2896: exact f32 overlaps in P6
   int64_t out;       // next clique index within the micrograph (fill)
   int64_t c0, c1;    // clique chunk being buffered in cbuf (fill)
   int64_t count;
@@ -484,7 +482,9 @@ __device__ __forceinline__ void fused_epilogue_order(const FCtx<K>& c, int64_t j
 #pragma unroll
     for (int b = a + 1; b < K; ++b) ji[a][b] = jaccard(xs[a], ys[a], xs[b], ys[b], c.B, c.two_b2);
   if (!c.set_order) {
+#ifndef RGC_X_NOINSKEY
     for (int i = 0; i < K; ++i) ins[i] = ins_key<K>(c, mem[i]);
+#endif
   }
   uint32_t top;
   int arg = epi_degree_max<K>(ji, &top);
@@ -1134,15 +1134,18 @@ void k_fused(FusedArgs A) {
   // coordinates is deferred to the f64 layout, where it is computed in f64)
   using BT = typename std::conditional<W, double, float>::type;
   BT bmnx = INFINITY, bmny = INFINITY, bmxx = -INFINITY, bmxy = -INFINITY;
-  bool inexact = false;   // a coordinate not exactly representable as f32 (NaN excepted)
-  bool nonint = false;    // a finite box with a coordinate off the integer grid (-2^23, 2^23)
+  // The f32 layout is the INTEGER layout: every finite coordinate an integer below 2^23 and
+  // an integer box size 1 <= B <= 2896, so P2's overlaps and P6's overlap products are exact
+  // floats (INTP); any other micrograph is deferred to the f64 ("wide") layout, whose kernel
+  // carries the f64 arithmetic.  (Real picker BOX files hold integer pixel coordinates.)
+  bool inexact = !W && !(A.B >= 1.0 && A.B <= 2896.0 && A.B == floor(A.B));
   each_box([&](int, double xv, double yv) {
     if (isfinite(xv) && isfinite(yv)) {
       bmnx = fmin(bmnx, (BT)xv); bmxx = fmax(bmxx, (BT)xv);
       bmny = fmin(bmny, (BT)yv); bmxy = fmax(bmxy, (BT)yv);
-      nonint |= xv != rint(xv) || yv != rint(yv) || fabs(xv) >= 0x1p23 || fabs(yv) >= 0x1p23;
+      if (!W)
+        inexact |= xv != rint(xv) || yv != rint(yv) || fabs(xv) >= 0x1p23 || fabs(yv) >= 0x1p23;
     }
-    if (!W) inexact |= ((double)(float)xv != xv && xv == xv) || ((double)(float)yv != yv && yv == yv);
   });
   if (inexact) bmnx = -INFINITY;   // (impossible otherwise) carried through the min reduction
   double mnx, mny, mxx, mxy;
@@ -1171,8 +1174,6 @@ void k_fused(FusedArgs A) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) H.red4[r][tid >> 6] = (double)bv[r];
     double v[4];
-    const bool wn = __any(nonint);
-    if ((tid & 63) == 0) H.nonint[tid >> 6] = wn ? 1 : 0;
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -1301,20 +1302,12 @@ void k_fused(FusedArgs A) {
   // band moves the quotient by >= 1.1e-12 relative), so the decision is the reference's.
   const double t_star = 0.6 * B * B / 1.3;
   const double i_lo = t_star * (1.0 - 0x1p-40), i_hi = t_star * (1.0 + 0x1p-40);
-  // integer coordinates (|v| < 2^23) and an integer 1 <= B <= 4095: the overlaps B - |dx| and
+  // f32 layout = integer coordinates (|v| < 2^23) and an integer 1 <= B <= 2896: the overlaps B - |dx| and
   // their product (< 2^24) are exact in f32 and JI > 0.3 <=> I > floor(6 B^2 / 13) (at
   // I = 6 B^2 / 13 the reference's quotient rounds to 0.3 itself, not above it), so the count
   // pass decides every candidate with six f32 operations (edge_test_int)
-  bool intp = false;
-  int ti = 0;
-  if (!W && B >= 1.0 && B <= 4095.0 && B == floor(B)) {
-    int nw = 0;
-#pragma unroll
-    for (int w = 0; w < FNW; ++w) nw |= H.nonint[w];
-    intp = nw == 0;
-    const int bi = (int)B;
-    ti = (6 * bi * bi) / 13;
-  }
+  // (the f32 layout is integer-only: P0)
+  const int ti = W ? 0 : (6 * (int)B * (int)B) / 13;
   // thread per box (sorted position): lanes of a wave hold neighbouring boxes of one picker,
   // so their stencils overlap (similar trip counts, broadcast LDS reads), and the waves of
   // picker K-1 have nothing to do.  cnt[] (dead until P3) keeps
@@ -1330,7 +1323,7 @@ void k_fused(FusedArgs A) {
     stencil_setup<K, W>(st, ts, S, G);
     uint32_t mask;
     int ec;
-    if (!W && intp) ec = pairs_count_int<K>(st, S, G, (float)B, (float)ti, &mask);
+    if constexpr (!W) ec = pairs_count_int<K>(st, S, G, (float)B, (float)ti, &mask);
     else ec = pairs_count<K, W>(st, S, G, B, two_b2, i_lo, i_hi, &mask);
     S.fwd[ts] = (uint16_t)ec;
     S.cnt[ts] = mask;
@@ -1576,7 +1569,9 @@ void k_fused(FusedArgs A) {
         int mem[K];
         mem[0] = r;
         c.count = 0;
+#ifndef RGC_X_NODFS
         FLevel<K, 1, false>::run(c, mem);
+#endif
         cntr = (uint32_t)c.count;
       }
       S.cnt[r] = cntr;
@@ -1672,7 +1667,6 @@ void k_fused(FusedArgs A) {
     // the DFS per chunk of <= cq_cap cliques.
     // scores of the clique vertices into LDS by row rank when they fit in parent..scell
     c.S.vstaged = 8 * H.V <= L.off_citems - L.off_parent;
-    c.intp = intp && A.B <= 2896.0;
     if (c.S.vstaged) {
       for (int t = tid; t < n; t += FWG)
         if (S.flags[t] == 3) c.S.vscore[S.vrank[t]] = c.score[b0 + S.citems[t]];
@@ -1718,7 +1712,9 @@ void k_fused(FusedArgs A) {
           int mem[K];
           mem[0] = r;
           c.out = lo;
+#ifndef RGC_X_NODFS
           FLevel<K, 1, true>::run(c, mem);
+#endif
         }
         __syncthreads();
       }
@@ -1741,7 +1737,7 @@ void k_fused(FusedArgs A) {
         continue;
 #endif
         bool order;
-        if (!W && c.intp) order = fused_epilogue_main<K, W, true>(c, obase + (c0 + sl), mem);
+        if constexpr (!W) order = fused_epilogue_main<K, W, true>(c, obase + (c0 + sl), mem);
         else order = fused_epilogue_main<K, W, false>(c, obase + (c0 + sl), mem);
         if (order) {
           c.cq_ord[sl] |= 0x8000;
