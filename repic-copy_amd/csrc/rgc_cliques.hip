@@ -372,7 +372,11 @@ __global__ __launch_bounds__(WG) void k5_epilogue(CliqueArgs A) {
     for (int i = 0; i < K; ++i) { xf[i] = (float)xs[i]; yf[i] = (float)ys[i]; }
     epi_core<K, float>(xf, yf, (float)B, two_b2, multi, &exact, &arg, &med);
   } else {
+#ifdef RGC_X_EPIF32ONLY
+    exact = true; med = 0.0;
+#else
     epi_core<K, double>(xs, ys, B, two_b2, multi, &exact, &arg, &med);
+#endif
   }
   A.w[j] = (float)((double)conf32 * med);
   A.conf[j] = conf32;

@@ -13,7 +13,7 @@ export TMPDIR=/tmp
 STEPS=3; WARM=1
 BENCH=(python3 bench.py --no-cpu-baseline --steps $STEPS --warmup $WARM --config "$CFG")
 if [ -n "$NMG" ]; then BENCH+=(--n_mg "$NMG"); fi
-KSUB=k_fused
+KSUB="k_fused<"
 if [ "$CFG" = "C5" ]; then KSUB=rgc::; fi
 pass() {  # name counters...
   local name=$1

@@ -14,7 +14,7 @@ for L in repic-copy_amd/repic_amd/ablate/librepic_gc_stop*.so repic-copy_amd/rep
     python3 tools/ablate.py "$CFG" "$NMG" 1 "$L" > "$OUT/$b.txt" 2> "$OUT/$b.err" || { tail -20 "$OUT/$b.err"; exit 1; }
   find "$OUT/$b" -name '*counter_collection.csv' -exec cp {} "$OUT/$b.csv" \;
   echo "== $b" | tee -a "$OUT/summary.log"
-  python3 tools/pmc_summary.py k_fused "$OUT/$b.csv" | tee -a "$OUT/summary.log"
+  python3 tools/pmc_summary.py "k_fused<" "$OUT/$b.csv" | tee -a "$OUT/summary.log"
 done
 python3 tools/pmc_ablate_delta.py "$OUT/summary.log" | tee "$OUT/delta.txt"
 echo "== done"
