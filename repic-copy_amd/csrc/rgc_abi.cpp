@@ -1036,9 +1036,47 @@ static int submit_fast(rgc_ctx* c, const rgc_batch_in* in) {
     nmaxb = std::max(nmaxb, nm);
   }
   if (nmaxb > FUSED_MAX_BOXES) return 0;
-  const FusedPlan& pl = cached_plan(k, 0, fused_class(nmaxb));
-  const FusedPlan& p0 = cached_plan(k, 0, fused_class(nmin));
-  if (!pl.nmax || p0.wg != pl.wg || p0.nt != pl.nt) return 0;
+  // launch groups: micrographs whose size classes share a plan's occupancy and workgroup
+  // size run as one launch at the group's largest class; several groups (C3 / C4 classes
+  // straddle an occupancy step) launch back to back over HBM micrograph lists, still without
+  // a host sync (deferrals show up in rgc_wait, which falls back to the general path)
+  struct Grp {
+    int wg, nt, cl;
+    std::vector<int32_t> mg;
+  };
+  std::vector<Grp> grp;
+  {
+    const FusedPlan& pl = cached_plan(k, 0, fused_class(nmaxb));
+    const FusedPlan& p0 = cached_plan(k, 0, fused_class(nmin));
+    if (!pl.nmax || !p0.nmax) return 0;
+    if (p0.wg == pl.wg && p0.nt == pl.nt) {
+      grp.push_back({pl.wg, pl.nt, fused_class(nmaxb), {}});
+    } else {
+      std::vector<std::pair<int, const FusedPlan*>> cp;   // few classes: linear cache
+      for (int m = 0; m < n_mg; ++m) {
+        const int cl = fused_class(in->box_off[(int64_t)(m + 1) * k] - in->box_off[(int64_t)m * k]);
+        const FusedPlan* p = nullptr;
+        for (const auto& e : cp)
+          if (e.first == cl) p = e.second;
+        if (!p) {
+          p = &cached_plan(k, 0, cl);
+          cp.push_back({cl, p});
+        }
+        if (!p->nmax) return 0;
+        Grp* g = nullptr;
+        for (auto& e : grp)
+          if (e.wg == p->wg && e.nt == p->nt) g = &e;
+        if (!g) {
+          grp.push_back({p->wg, p->nt, cl, {}});
+          g = &grp.back();
+        }
+        g->cl = std::max(g->cl, cl);
+        g->mg.push_back(m);
+      }
+      for (const auto& g : grp)   // the group's largest class must keep its occupancy
+        if (cached_plan(k, 0, g.cl).wg != g.wg || cached_plan(k, 0, g.cl).nt != g.nt) return 0;
+    }
+  }
   const bool multi = (flags & RGC_F_MULTI_OUT) != 0;
   const bool want_members = (flags & (RGC_F_MEMBERS | RGC_F_MULTI_OUT)) != 0;
   hipStream_t s = c->stream;
@@ -1066,17 +1104,39 @@ static int submit_fast(rgc_ctx* c, const rgc_batch_in* in) {
   A.order = multi ? D<uint8_t>(c, D_ORDER) : nullptr;
   A.stamps = nullptr;
   A.eu = nullptr; A.ev = nullptr; A.eji = nullptr; A.ecap_out = 0;
-  A.nmax = pl.nmax; A.ecap = pl.ecap; A.mg_list = nullptr;
+  A.mg_list = nullptr;
   A.tie_list = D<int32_t>(c, D_TIES);
   A.tie_cap = c->cap_cliques;
 #ifdef RGC_STAMPS
   return 0;   // the diagnostic build times through rgc_run only
 #endif
-  TRY(ensure_qg(c, A, k, pl.nt));
-  TRY(mark(c, "k_fused"));
-  const int le = launch_fused(s, n_mg, pl.lds, A, false, pl.nt);
-  if (le != 0) return fail("fused kernel launch failed (submit): " +
-                           std::string(le > 0 ? hipGetErrorString((hipError_t)le) : "unsupported k"));
+  int32_t* d_ml = nullptr;
+  if (grp.size() > 1) {   // micrograph lists, group after group, through the pinned stage
+    TRY(ensure_host(c, H_FSTAGE, (size_t)n_mg * 4));
+    TRY(ensure_dev(c, D_MGLIST, (size_t)n_mg * 4));
+    int32_t* h_ml = H<int32_t>(c, H_FSTAGE);
+    size_t o = 0;
+    for (const auto& g : grp) {
+      std::memcpy(h_ml + o, g.mg.data(), g.mg.size() * 4);
+      o += g.mg.size();
+    }
+    d_ml = D<int32_t>(c, D_MGLIST);
+    HIPCHK(hipMemcpyAsync(d_ml, h_ml, (size_t)n_mg * 4, hipMemcpyHostToDevice, s));
+  }
+  size_t o = 0;
+  for (const auto& g : grp) {
+    const FusedPlan& pl = cached_plan(k, 0, g.cl);
+    const int nb = grp.size() > 1 ? (int)g.mg.size() : n_mg;
+    A.nmax = pl.nmax;
+    A.ecap = pl.ecap;
+    A.mg_list = grp.size() > 1 ? d_ml + o : nullptr;
+    o += g.mg.size();
+    TRY(ensure_qg(c, A, k, pl.nt));
+    TRY(mark(c, "k_fused"));
+    const int le = launch_fused(s, nb, pl.lds, A, false, pl.nt);
+    if (le != 0) return fail("fused kernel launch failed (submit): " +
+                             std::string(le > 0 ? hipGetErrorString((hipError_t)le) : "unsupported k"));
+  }
   TRY(mark(c, "k_fused_ties"));
   if (launch_fused_ties(s, A, 0) != 0) return fail("tie kernel launch failed (submit)");
   c->pend_slot = io.slot;
