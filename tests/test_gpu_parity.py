@@ -149,6 +149,30 @@ def test_gpu_dense_clusters_match_oracle(k, per, n_clusters):
     _check_vs_oracle(mgs, k, 100, no_fused=True)
 
 
+@pytest.mark.parametrize("box,shift,frac", [(64, 0, False), (255, 0, False), (256, 0, False),
+                                             (300, 0, False), (100, 0, True), (100, 18000, False),
+                                             (100, -17000, False)])
+def test_gpu_large_route_epilogue_paths(box, shift, frac):
+    """k5_epilogue's paths on the multi-kernel route: packed-u16 clique pairs (integer
+    coordinates in [-16384, 16383], integer B <= 255), one float clique at a time (B > 255,
+    or a pair with a partner outside that range), f64 (fractional coordinates); odd and even
+    clique counts."""
+    mgs = []
+    for seed in range(3):
+        mg = _dense_clusters(4, 3, 9 + seed, seed, box=box)
+        out = []
+        for p, (x, y, s) in enumerate(mg):
+            x, y = x.copy(), y.copy()
+            if shift:
+                x[: len(x) // 3] += shift   # some clusters out of the u16 range
+            if frac and p == 1:
+                x += 0.5
+            out.append((x, y, s))
+        mgs.append(out)
+    _check_vs_oracle(mgs, 4, box, no_fused=True)
+    _check_vs_oracle(mgs, 4, box, no_fused=True, get_cc=True)
+
+
 def test_gpu_full_c2_properties():
     """Full BASELINE config #2 (10k micrographs): size-independent invariants."""
     from repic_amd import _lib, synth
