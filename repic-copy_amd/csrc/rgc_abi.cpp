@@ -491,7 +491,7 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   A.adjg = D<uint64_t>(c, D_ADJG); A.rbound = D<uint64_t>(c, D_RBOUND);
   A.rflag = D<uint8_t>(c, D_RFLAG); A.dfs_mg = D<uint8_t>(c, D_DFSMG); A.dfs_base = 0;
   A.root_box = D<int32_t>(c, D_ROOTBOX);
-  A.exlist = nullptr; A.excount = nullptr;
+  A.exmask = nullptr; A.exlist = nullptr; A.excount = nullptr;
   A.members = nullptr; A.rows = nullptr; A.w = nullptr; A.conf = nullptr; A.consensus = nullptr;
   A.order = nullptr;
   int64_t* d_tot = D<int64_t>(c, D_TOTAL);   // [0] edges, [1] DFS cliques, [2] level, [3] rank
@@ -564,16 +564,19 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   launch_clique_level(s, k == 2, true, true, A, L);
   TRY(mark(c, "k5_dfs_fill"));
   launch_cliques_dfs(s, true, (int)N, A);
-  TRY(ensure_dev(c, D_EXLIST, C * 8));
+  TRY(ensure_dev(c, D_EXLIST, (C + (C + 63) / 64) * 8));
   A.exlist = D<int64_t>(c, D_EXLIST);
+  A.exmask = reinterpret_cast<uint64_t*>(A.exlist + C);
   A.excount = reinterpret_cast<unsigned long long*>(d_tot + 3);   // rank scan total is dead
   HIPCHK(hipMemsetAsync(A.excount, 0, 8, s));
-  TRY(ensure_dev(c, D_PK, (size_t)N * 32));
+  TRY(ensure_dev(c, D_PK, (size_t)N * 16));
   A.pk = D<double>(c, D_PK);
   TRY(mark(c, "k5_pack"));
   launch_clique_pack(s, (int)N, A);
   TRY(mark(c, "k5_epilogue"));
-  launch_clique_epilogue(s, A);
+  launch_clique_epilogue(s, false, A);
+  TRY(mark(c, "k5_epi_exact"));
+  launch_clique_epilogue(s, true, A);
   TRY(mark(c, "k5_ranges"));
   launch_clique_ranges(s, A, C1, D<int64_t>(c, D_RLO), D<int64_t>(c, D_RLO) + n_mg);
   HIPCHK(hipMemcpyAsync(H<void>(c, H_STAT), D<void>(c, D_STAT), n_mg * sizeof(MgStat),

@@ -264,7 +264,11 @@ __device__ __forceinline__ void epi_core(const T (&xs)[K], const T (&ys)[K], T B
           I[t++] = overlap(xs[a], ys[a], xs[b], ys[b], B);
       }
   }
+#ifdef RGC_X_EPI_NODEG
+  if (false) {
+#else
   if (!multi) {
+#endif
     // weighted degrees from f32 JIs: f32 operands (2^-24 each) and v_rcp_f32 (1 ulp) give
     // < 4e-7 per JI <= 1, < 5.5e-6 per sum of <= 7 terms with its f32 additions; a maximum
     // clear by 3e-5 is the reference's, anything closer takes the exact f64 pass (ties)
@@ -302,7 +306,14 @@ __device__ __forceinline__ void epi_core(const T (&xs)[K], const T (&ys)[K], T B
 #pragma unroll
     for (int t = 0; t < NE; ++t) nan |= isnan(I[t]);
   }
+#ifdef RGC_X_EPI_NOMED
+  { T acc = I[0];
+#pragma unroll
+    for (int t = 1; t < NE; ++t) acc = acc + I[t];
+    I[NE / 2] = I[NE / 2 - 1] = acc; }
+#else
   mid_n<NE>(I);
+#endif
   if (NE & 1) {
     const double m = (double)I[NE / 2];
     *med = nan ? NAN : m / (two_b2 - m);
@@ -312,84 +323,242 @@ __device__ __forceinline__ void epi_core(const T (&xs)[K], const T (&ys)[K], T B
   }
 }
 
-// One 32-byte record per box for the epilogue's member gathers (x, y, score, row rank in the
-// low word of the last slot): two 16-byte loads per member instead of four scattered ones.
+// One 16-byte record per box for the epilogue's member gathers: the score, the row rank and,
+// for integer coordinates in [-16384, 16383], both coordinates biased by 2^14 as u16s below
+// 2^15 (0xffffffff otherwise: that clique takes the f64 path from A.x / A.y).  One 16-byte
+// load per member and no per-clique integrality tests.
 __global__ __launch_bounds__(WG) void k5_pack(int N, CliqueArgs A) {
   const int i = blockIdx.x * WG + threadIdx.x;
   if (i >= N) return;
-  double2* o = reinterpret_cast<double2*>(A.pk) + 2 * (int64_t)i;
-  o[0] = make_double2(A.x[i], A.y[i]);
-  o[1] = make_double2(A.score[i], __longlong_as_double((long long)(uint32_t)A.vrow[i]));
+  const double x = A.x[i], y = A.y[i];
+  uint32_t xy = 0xffffffffu;
+  if (x == rint(x) && y == rint(y) && x >= -16384.0 && x <= 16383.0 && y >= -16384.0 &&
+      y <= 16383.0)
+    xy = (uint32_t)((int)x + 16384) | ((uint32_t)((int)y + 16384) << 16);
+  const uint64_t ry = (uint64_t)(uint32_t)A.vrow[i] | ((uint64_t)xy << 32);
+  reinterpret_cast<double2*>(A.pk)[i] = make_double2(A.score[i], __longlong_as_double((long long)ry));
 }
 
-// ILP epilogue, one thread per clique (get_cliques.py:164-202): COO rows (vertex ranks by
-// (x, y, id), ascending), conf = f32(median score), w = f32(f64(conf) * median JI), and the
-// consensus box (largest weighted degree, CPython set-order tie-break); --multi_out: the
-// networkx node-iteration order of the members.  Same arithmetic as the fused kernel's
-// epilogue (rgc_fused.hip fused_epilogue_main / _order).
+// Member gathers of one clique: COO rows (vertex ranks by (x, y, id), ascending) stored,
+// conf = f32(median score), the packed coordinates for the overlap paths.
 template <int K>
-__global__ __launch_bounds__(WG) void k5_epilogue(CliqueArgs A) {
-  constexpr int NE = K * (K - 1) / 2;
-  const int64_t j = (int64_t)blockIdx.x * WG + threadIdx.x;
-  if (j >= A.C) return;
-  int mem[K];
+__device__ __forceinline__ void epi_gather(const CliqueArgs& A, int64_t j, int (&mem)[K],
+                                           uint32_t (&xy)[K], float* conf32) {
 #pragma unroll
   for (int i = 0; i < K; ++i) mem[i] = A.members[j * K + i];
-  double xs[K], ys[K];
-  float conf32;
-  {
-    double s[K];
-    int r[K];
+  double s[K];
+  int r[K];
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
-      const double2* pk = reinterpret_cast<const double2*>(A.pk) + 2 * (int64_t)mem[i];
-      const double2 p0 = pk[0], p1 = pk[1];
-      xs[i] = p0.x;
-      ys[i] = p0.y;
-      s[i] = p1.x;
-      r[i] = (int)(uint32_t)__double_as_longlong(p1.y);
-    }
-    cmpnet_apply<K, false>(r);   // ascending rows
-#pragma unroll
-    for (int i = 0; i < K; ++i) A.rows[j * K + i] = r[i];
-    conf32 = (float)median_n<K>(s);   // conf = f32(median score)
+  for (int i = 0; i < K; ++i) {
+    const double2 p = reinterpret_cast<const double2*>(A.pk)[mem[i]];
+    const uint64_t ry = (uint64_t)__double_as_longlong(p.y);
+    s[i] = p.x;
+    r[i] = (int)(uint32_t)ry;
+    xy[i] = (uint32_t)(ry >> 32);
   }
+  cmpnet_apply<K, false>(r);   // ascending rows
+#pragma unroll
+  for (int i = 0; i < K; ++i) A.rows[j * K + i] = r[i];
+  *conf32 = (float)median_n<K>(s);   // conf = f32(median score)
+}
+
+// One clique's weighted-degree candidate and median JI: exact floats for integer coordinates
+// (k5_pack) and integer B <= 2896 (as the fused epilogue's INTP path), f64 otherwise.
+template <int K>
+__device__ __forceinline__ void epi_single(const CliqueArgs& A, const int (&mem)[K],
+                                           const uint32_t (&xy)[K], bool multi, bool* exact,
+                                           int* arg, double* med) {
   const double B = A.B, two_b2 = A.two_b2;
-  const bool multi = (A.flags & 2) != 0;
-  int arg = 0;
-  bool exact = multi;
-  double med;
-  // integer coordinates below 2^23 and B <= 2896: overlaps, their median network and the
-  // degree JIs on exact floats (as the fused epilogue's INTP path); otherwise f64
   bool intok = B >= 1.0 && B <= 2896.0 && B == floor(B);
 #pragma unroll
-  for (int i = 0; i < K; ++i)
-    intok = intok && xs[i] == rint(xs[i]) && ys[i] == rint(ys[i]) && fabs(xs[i]) < 0x1p23 &&
-            fabs(ys[i]) < 0x1p23;
+  for (int i = 0; i < K; ++i) intok = intok && xy[i] != 0xffffffffu;
   if (intok) {
     float xf[K], yf[K];
 #pragma unroll
-    for (int i = 0; i < K; ++i) { xf[i] = (float)xs[i]; yf[i] = (float)ys[i]; }
-    epi_core<K, float>(xf, yf, (float)B, two_b2, multi, &exact, &arg, &med);
+    for (int i = 0; i < K; ++i) {   // 2^23 + u: exact, and differences stay float ops
+      xf[i] = __uint_as_float(0x4b000000u | (xy[i] & 0xffffu));
+      yf[i] = __uint_as_float(0x4b000000u | (xy[i] >> 16));
+    }
+    epi_core<K, float>(xf, yf, (float)B, two_b2, multi, exact, arg, med);
   } else {
 #ifdef RGC_X_EPIF32ONLY
-    exact = true; med = 0.0;
+    *exact = true; *med = 0.0;   // timing experiment: the f64 path's registers out
 #else
-    epi_core<K, double>(xs, ys, B, two_b2, multi, &exact, &arg, &med);
+    double xs[K], ys[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) { xs[i] = A.x[mem[i]]; ys[i] = A.y[mem[i]]; }
+    epi_core<K, double>(xs, ys, B, two_b2, multi, exact, arg, med);
 #endif
   }
-  A.w[j] = (float)((double)conf32 * med);
-  A.conf[j] = conf32;
-  if (exact) {
-    // the rare cliques that need exact f64 degrees / node order: second kernel (its 64-bit
-    // hashing and K x K JIs stay out of this kernel's register budget)
-    A.exlist[atomicAdd(A.excount, 1ull)] = j;
-    return;
-  }
-  int cons = mem[0];
+}
+
+// Two cliques at once for integer coordinates and integer B <= 255: every overlap
+// max(B - |dx|, 0) * max(B - |dy|, 0) <= 65025 is an exact u16, so the overlaps and their
+// median network run on packed u16 pairs (v_pk_sub/min/mul_lo_u16, v_pk_min/max_u16; the
+// biased coordinates are below 2^15, so u16 differences never wrap past B).  Degrees and
+// median JIs per clique exactly as epi_core's float path.
+template <int K>
+__device__ __forceinline__ void epi_pair(const uint32_t (&xy0)[K], const uint32_t (&xy1)[K],
+                                         uint32_t b16, double two_b2, bool multi, bool* ex,
+                                         int* arg, double* med) {
+  constexpr int NE = K * (K - 1) / 2;
+  u16x2 X[K], Y[K];
 #pragma unroll
-  for (int i = 1; i < K; ++i) cons = (arg == i) ? mem[i] : cons;
-  A.consensus[j] = cons;
+  for (int i = 0; i < K; ++i) {
+    X[i] = __builtin_bit_cast(u16x2, (xy0[i] & 0xffffu) | (xy1[i] << 16));
+    Y[i] = __builtin_bit_cast(u16x2, (xy0[i] >> 16) | (xy1[i] & 0xffff0000u));
+  }
+  const u16x2 Bv = __builtin_bit_cast(u16x2, b16 | (b16 << 16));
+  u16x2 I[NE];
+  {
+    int t = 0;
+#pragma unroll
+    for (int a = 0; a < K; ++a)
+#pragma unroll
+      for (int b = a + 1; b < K; ++b) {
+        const u16x2 ox = __builtin_elementwise_sub_sat(
+            Bv, __builtin_elementwise_min(X[a] - X[b], X[b] - X[a]));
+        const u16x2 oy = __builtin_elementwise_sub_sat(
+            Bv, __builtin_elementwise_min(Y[a] - Y[b], Y[b] - Y[a]));
+        I[t++] = ox * oy;
+      }
+  }
+  if (!multi) {
+    const float c = (float)two_b2;
+    float d0[K], d1[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) { d0[i] = 0.0f; d1[i] = 0.0f; }
+    int t = 0;
+#pragma unroll
+    for (int a = 0; a < K; ++a)
+#pragma unroll
+      for (int b = a + 1; b < K; ++b) {
+        const float i0 = (float)I[t].x, i1 = (float)I[t].y;
+        const float j0 = i0 * __builtin_amdgcn_rcpf(c - i0);
+        const float j1 = i1 * __builtin_amdgcn_rcpf(c - i1);
+        d0[a] += j0; d0[b] += j0;
+        d1[a] += j1; d1[b] += j1;
+        ++t;
+      }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      float m1 = q ? d1[0] : d0[0], m2 = -INFINITY;
+      int ag = 0;
+#pragma unroll
+      for (int i = 1; i < K; ++i) {
+        const float d = q ? d1[i] : d0[i];
+        m2 = d > m1 ? m1 : fmaxf(m2, d);
+        ag = d > m1 ? i : ag;
+        m1 = fmaxf(m1, d);
+      }
+      arg[q] = ag;
+      ex[q] = !(m1 - m2 > 3e-5f);   // epi_core's margin
+    }
+  }
+  mid_n<NE>(I);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if (NE & 1) {
+      const double m = (double)(q ? I[NE / 2].y : I[NE / 2].x);
+      med[q] = m / (two_b2 - m);
+    } else {
+      const double a = (double)(q ? I[NE / 2 - 1].y : I[NE / 2 - 1].x);
+      const double b = (double)(q ? I[NE / 2].y : I[NE / 2].x);
+      med[q] = ((a / (two_b2 - a)) + (b / (two_b2 - b))) / 2.0;
+    }
+  }
+}
+
+// spread the low 32 bits of v to the even bit positions of a 64-bit word
+__device__ __forceinline__ uint64_t spread_even(uint64_t v) {
+  v &= 0xffffffffull;
+  v = (v | (v << 16)) & 0x0000ffff0000ffffull;
+  v = (v | (v << 8)) & 0x00ff00ff00ff00ffull;
+  v = (v | (v << 4)) & 0x0f0f0f0f0f0f0f0full;
+  v = (v | (v << 2)) & 0x3333333333333333ull;
+  v = (v | (v << 1)) & 0x5555555555555555ull;
+  return v;
+}
+
+// ILP epilogue, two cliques per thread (get_cliques.py:164-202): COO rows, conf = f32(median
+// score), w = f32(f64(conf) * median JI), and the consensus box (largest weighted degree,
+// CPython set-order tie-break); --multi_out: the networkx node-iteration order of the members.
+// Same arithmetic as the fused kernel's epilogue (rgc_fused.hip fused_epilogue_main / _order).
+// Thread t takes cliques 2t and 2t + 1: the packed-u16 pair path when both qualify, one at a
+// time otherwise.
+template <int K>
+__global__ __launch_bounds__(WG) void k5_epilogue(CliqueArgs A) {
+  const int64_t j0 = 2 * ((int64_t)blockIdx.x * WG + threadIdx.x);
+  if (j0 >= A.C) return;
+  const bool two = j0 + 1 < A.C;
+  int mem0[K], mem1[K];
+  uint32_t xy0[K], xy1[K];
+  float cf0, cf1 = 0.0f;
+  epi_gather<K>(A, j0, mem0, xy0, &cf0);
+  if (two) epi_gather<K>(A, j0 + 1, mem1, xy1, &cf1);
+  const double B = A.B;
+  const bool multi = (A.flags & 2) != 0;
+  bool ex[2] = {multi, multi};
+  int arg[2] = {0, 0};
+  double med[2] = {0.0, 0.0};
+  bool pair = two && B >= 1.0 && B <= 255.0 && B == floor(B);
+#pragma unroll
+  for (int i = 0; i < K; ++i) pair = pair && xy0[i] != 0xffffffffu && xy1[i] != 0xffffffffu;
+  if (pair) {
+    epi_pair<K>(xy0, xy1, (uint32_t)B, A.two_b2, multi, ex, arg, med);
+  } else {
+    epi_single<K>(A, mem0, xy0, multi, &ex[0], &arg[0], &med[0]);
+    if (two) epi_single<K>(A, mem1, xy1, multi, &ex[1], &arg[1], &med[1]);
+  }
+  A.w[j0] = (float)((double)cf0 * med[0]);
+  A.conf[j0] = cf0;
+  if (two) {
+    A.w[j0 + 1] = (float)((double)cf1 * med[1]);
+    A.conf[j0 + 1] = cf1;
+  }
+  // the cliques that need exact f64 degrees / node order (~3 % on C5, i.e. most waves hold
+  // one): k5_ex_compact + k5_epi_exact, their 64-bit hashing and K x K JIs out of this
+  // kernel's register budget.  Ballot words, bit j & 63 of word j >> 6: this wave's 128
+  // cliques are words 2w (lanes 0-31) and 2w + 1 (lanes 32-63), no global atomics.
+  const uint64_t b0 = __ballot(ex[0]), b1 = __ballot(ex[1] && two);
+  if ((threadIdx.x & 63) == 0) {
+    A.exmask[j0 >> 6] = spread_even(b0) | (spread_even(b1) << 1);
+    if (j0 + 64 < A.C)
+      A.exmask[(j0 >> 6) + 1] = spread_even(b0 >> 32) | (spread_even(b1 >> 32) << 1);
+  }
+  if (!ex[0]) {
+    int cons = mem0[0];
+#pragma unroll
+    for (int i = 1; i < K; ++i) cons = (arg[0] == i) ? mem0[i] : cons;
+    A.consensus[j0] = cons;
+  }
+  if (two && !ex[1]) {
+    int cons = mem1[0];
+#pragma unroll
+    for (int i = 1; i < K; ++i) cons = (arg[1] == i) ? mem1[i] : cons;
+    A.consensus[j0 + 1] = cons;
+  }
+}
+
+// The deferred cliques as a list: one wave per 64 ballot words (4096 cliques) ranks their set
+// bits with a DPP scan of the word popcounts and reserves its slice of the list with one
+// atomic (C / 4096 atomics per launch instead of one per epilogue wave).
+__global__ __launch_bounds__(WG) void k5_ex_compact(CliqueArgs A) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwords = (A.C + 63) >> 6;
+  const int64_t w0 = (((int64_t)blockIdx.x * WG + threadIdx.x) >> 6) * 64;
+  if (w0 >= nwords) return;   // wave-uniform
+  const uint64_t word = w0 + lane < nwords ? A.exmask[w0 + lane] : 0ull;
+  const int cnt = __popcll(word);
+  const int incl = wave_incl_add32(cnt);
+  const int total = __shfl(incl, 63);
+  if (total == 0) return;
+  unsigned long long base = 0;
+  if (lane == 0) base = atomicAdd(A.excount, (unsigned long long)total);
+  base = ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(base >> 32), 0) << 32) |
+         (uint32_t)__shfl((int)(uint32_t)base, 0);
+  int64_t o = (int64_t)base + incl - cnt;
+  for (uint64_t w = word; w; w &= w - 1) A.exlist[o++] = ((w0 + lane) << 6) + __builtin_ctzll(w);
 }
 
 // Consensus (and --multi_out node order) of the cliques k5_epilogue deferred: exact f64
@@ -484,15 +653,22 @@ void launch_clique_setup(hipStream_t stream, int N, const CliqueArgs& A) {
   if (nr) hipLaunchKernelGGL(k5n_build, dim3((nr + WG / NBG - 1) / (WG / NBG)), dim3(WG), 0, stream, A);
 }
 
-int launch_clique_epilogue(hipStream_t stream, const CliqueArgs& A) {
+#ifndef RGC_EXGRID
+#define RGC_EXGRID 1024
+#endif
+int launch_clique_epilogue(hipStream_t stream, bool exact_pass, const CliqueArgs& A) {
   const int64_t nb = (A.C + WG - 1) / WG;
   if (nb <= 0) return 0;
   switch (A.k) {
-#define RGC_EPI(KK)                                                                     \
-  case KK:                                                                              \
-    hipLaunchKernelGGL((k5_epilogue<KK>), dim3(nb), dim3(WG), 0, stream, A);            \
-    hipLaunchKernelGGL((k5_epi_exact<KK>), dim3(std::min<int64_t>(nb, 1024)), dim3(WG), 0, \
-                       stream, A);                                                      \
+#define RGC_EPI(KK)                                                                      \
+  case KK:                                                                               \
+    if (!exact_pass)                                                                     \
+      hipLaunchKernelGGL((k5_epilogue<KK>), dim3((nb + 1) / 2), dim3(WG), 0, stream, A); \
+    else {                                                                               \
+      hipLaunchKernelGGL(k5_ex_compact, dim3((nb + 63) / 64), dim3(WG), 0, stream, A);   \
+      hipLaunchKernelGGL((k5_epi_exact<KK>), dim3(std::min<int64_t>(nb, RGC_EXGRID)),      \
+                         dim3(WG), 0, stream, A);                                        \
+    }                                                                                    \
     break;
     RGC_EPI(2) RGC_EPI(3) RGC_EPI(4) RGC_EPI(5) RGC_EPI(6) RGC_EPI(7) RGC_EPI(8)
 #undef RGC_EPI

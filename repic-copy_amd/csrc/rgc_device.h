@@ -374,6 +374,11 @@ __host__ __device__ __forceinline__ float cmp_lo(float x, float y) { return fmin
 __host__ __device__ __forceinline__ float cmp_hi(float x, float y) { return fmaxf(x, y); }
 __host__ __device__ __forceinline__ int cmp_lo(int x, int y) { return x < y ? x : y; }
 __host__ __device__ __forceinline__ int cmp_hi(int x, int y) { return x < y ? y : x; }
+// two u16 lanes per register (v_pk_min_u16 / v_pk_max_u16): the large-route epilogue's
+// clique pairs (rgc_cliques.hip k5_epilogue)
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 cmp_lo(u16x2 x, u16x2 y) { return __builtin_elementwise_min(x, y); }
+__device__ __forceinline__ u16x2 cmp_hi(u16x2 x, u16x2 y) { return __builtin_elementwise_max(x, y); }
 template <int N, bool WANT_MID, typename T>
 __host__ __device__ __forceinline__ void cmpnet_apply(T (&v)[N]) {
   constexpr int n = CmpNetOf<N, WANT_MID>::net.n;

@@ -170,7 +170,9 @@ struct CliqueArgs {
   uint8_t* rflag;            // [N] root enumerated by the level kernels
   uint8_t* dfs_mg;           // [n_mg] micrograph takes the DFS route (a root > RB_W nbrs)
   int32_t* root_box;         // [n_roots] box of each picker-0 root
-  int64_t* exlist;           // [C] epilogue: cliques deferred to the exact pass
+  uint64_t* exmask;          // [ceil(C / 64)] epilogue: cliques deferred to the exact pass (one
+                             // ballot word per epilogue wave) ...
+  int64_t* exlist;           // [C] ... and as a list (k5_ex_compact)
   unsigned long long* excount;
   int64_t dfs_base;          // first output clique of the DFS route
   int32_t* members;
@@ -216,7 +218,7 @@ struct LevelArgs {
 void launch_clique_setup(hipStream_t stream, int N, const CliqueArgs& A);
 int launch_clique_level(hipStream_t stream, bool first, bool leaf, bool fill, const CliqueArgs& A,
                         const LevelArgs& L);
-int launch_clique_epilogue(hipStream_t stream, const CliqueArgs& A);
+int launch_clique_epilogue(hipStream_t stream, bool exact_pass, const CliqueArgs& A);
 void launch_clique_pack(hipStream_t stream, int N, const CliqueArgs& A);
 void launch_clique_ranges(hipStream_t stream, const CliqueArgs& A, int64_t C1, int64_t* rlo,
                           int64_t* rhi);
