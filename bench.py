@@ -270,58 +270,63 @@ def self_launch(n):
         time.sleep(0.05)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="C2")
-    ap.add_argument("--n_mg", type=int, default=None, help="micrographs per GPU")
-    ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--host-io", action="store_true",
-                    help="PCIe-inclusive variant (never the headline value): host x/y/score and "
-                         "offsets are uploaded and every per-clique output is copied back to "
-                         "pinned host memory inside each step")
-    ap.add_argument("--no-pipeline", action="store_true",
-                    help="synchronous rgc_run per step instead of two contexts in flight")
-    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
-    args = ap.parse_args()
+def derived_bound(rec, kernel, alg_bytes, kernel_ms, dv_kernel="k_fused"):
+    """The roofline class the counters put this kernel in (the same evidence as ``limiter``):
+    "hbm" when the measured HBM bandwidth is >= 50 % of peak, "valu" when the VALU pipe is
+    busy > 60 % of the time, "latency" otherwise; "unmeasured" without counters for this
+    library build.  Throughput is priced against HBM either way (no contraction, no MFMA).
+    The issue counters are those of ``dv_kernel`` (the multi-kernel route: its longest
+    kernel)."""
+    if rec is None:
+        return "unmeasured"
+    traffic, hbm, _ = roofline_evidence(rec, kernel, alg_bytes, kernel_ms)
+    if hbm is None:
+        return "unmeasured"
+    dv = rec.get("kernels", {}).get(dv_kernel, {}).get("derived", {})
+    if hbm >= 0.5:
+        return "hbm"
+    if dv.get("valu_busy", 0.0) > 0.6:
+        return "valu"
+    return "latency" if dv else "unmeasured"
 
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(self_launch(args.gpus))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus:
-        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
-    if args.launch_check:   # test hook: the launcher's rank layout, no GPU work
-        print(json.dumps({k_: os.environ.get(k_) for k_ in
-                          ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR")}), flush=True)
-        return
 
+class Env:
+    """Rank layout and devices of this bench process (one GPU per rank over RCCL)."""
+
+    def __init__(self, args):
+        import torch
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        # RGC_BENCH_DEVICE / RGC_DIST_BACKEND: test hooks (two ranks on one GPU over gloo);
+        # the driver's runs use one GPU per rank over RCCL ("nccl")
+        self.local = int(os.environ.get("RGC_BENCH_DEVICE", local))
+        self.backend = os.environ.get("RGC_DIST_BACKEND", "nccl")
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            torch.cuda.set_device(self.local)
+            if self.backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            else:
+                dist.init_process_group(self.backend)
+            self.dist = dist
+        self.dev = torch.device("cuda", self.local)
+        # collective tensors
+        self.cdev = self.dev if self.backend == "nccl" else torch.device("cpu")
+
+
+def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=False):
+    """Time ``steps`` steps of the hot path over one synthetic batch of ``config`` (n_mg
+    micrographs per rank, inputs resident in HBM): barrier + synchronize on both sides, max
+    over ranks.  Returns (report dict, cfg, this rank's micrographs)."""
     import torch
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # RGC_BENCH_DEVICE / RGC_DIST_BACKEND: test hooks (two ranks on one GPU over gloo);
-    # the driver's runs use one GPU per rank over RCCL ("nccl")
-    local = int(os.environ.get("RGC_BENCH_DEVICE", local))
-    backend = os.environ.get("RGC_DIST_BACKEND", "nccl")
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-    dev = torch.device("cuda", local)
-    cdev = dev if backend == "nccl" else torch.device("cpu")   # collective tensors
 
     from repic_amd import _lib, synth
     from repic_amd.pipeline import Batch
 
-    cfg = synth.SynthConfig(**synth.CONFIGS[args.config], seed=args.seed)
-    n_mg = args.n_mg or DEFAULT_MG[args.config]
+    dist, world, rank, dev, cdev = env.dist, env.world, env.rank, env.dev, env.cdev
+    cfg = synth.SynthConfig(**synth.CONFIGS[config], seed=args.seed)
     t_gen = time.time()
     mgs = synth.batch(cfg, n_mg, start=rank * n_mg)    # this rank's shard of one big batch
     batch = Batch.pack(cfg.k, cfg.box, mgs)
@@ -348,17 +353,17 @@ def main():
     # kernels concurrently: more throughput, but per-launch kernel times that overlap)
     tstream = torch.cuda.Stream(dev)
     stream = tstream.cuda_stream
-    ctx = _lib.Context(local, stream)
+    ctx = _lib.Context(env.local, stream)
     flags = _lib.F_DEVICE_INPUTS
     # pipelined steps (default): two contexts on that one stream, rgc_submit / rgc_wait, so the
     # host side of step i+1 (planning, launch) overlaps the device work of step i while the
     # kernels stay serialised; every step runs the whole hot path into its own context's
     # outputs and is waited for
-    pipeline = not (args.host_io or args.no_pipeline)
-    ctxs = [ctx, _lib.Context(local, stream)] if pipeline else [ctx]
+    pipeline = not (host_io or no_pipeline)
+    ctxs = [ctx, _lib.Context(env.local, stream)] if pipeline else [ctx]
 
     def step(timing=False):
-        if args.host_io:
+        if host_io:
             return ctx.run(batch.n_mg, cfg.k, cfg.box, batch.box_off, batch.id_base,
                            batch.x, batch.y, batch.score,
                            _lib.F_HOST_OUTPUTS | (_lib.F_TIMING if timing else 0))
@@ -394,20 +399,24 @@ def main():
                     ktimes[name] = ktimes.get(name, 0.0) + ms
         return r
 
-    if args.warmup:
-        steps_run(args.warmup, False)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ktimes = {}
-    r = steps_run(args.steps, True, ktimes)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    N, E, C = int(r.n_boxes), int(r.n_edges), int(r.n_cliques)
-    V = int(r.n_vert.sum())
+    try:
+        if warmup:
+            steps_run(warmup, False)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ktimes = {}
+        r = steps_run(steps, True, ktimes)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        N, E, C = int(r.n_boxes), int(r.n_edges), int(r.n_cliques)
+        V = int(r.n_vert.sum())
+    finally:
+        for c in ctxs:
+            c.close()
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -419,7 +428,6 @@ def main():
     else:
         tot_mg, tot_e, tot_c = n_mg, E, C
 
-    steps = args.steps
     value = tot_mg * steps / elapsed
     avg = {k_: v / steps for k_, v in ktimes.items()}
     dev_ms = sum(v for k_, v in avg.items() if k_ not in ("d2h", "h2d_meta", "d2h_stats"))
@@ -437,26 +445,25 @@ def main():
         dom_bytes = pipe
         dom_ms = dev_ms
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    rec, traffic_src = pmc_record(args.config)
-    traffic, hbm_frac, limiter = roofline_evidence(rec, "k_fused" if dom == "k_fused" else "route",
-                                                   dom_bytes, dom_ms)
+    rec, traffic_src = pmc_record(config)
+    kind = "k_fused" if dom == "k_fused" else "route"
+    traffic, hbm_frac, limiter = roofline_evidence(rec, kind, dom_bytes, dom_ms)
     out = {
-        "metric": "micrographs/sec (get_cliques, whole node) at 1/2/4/8 MI355X; % HBM roofline",
         "value": value, "unit": "micrographs/s", "n_gpus": world, "steps": steps,
-        "warmup": args.warmup, "ms_per_step": elapsed / steps * 1e3,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "f64", "data": "synthetic (seeded SURVEY.md §8(d) generator)",
-        "config": {"workload": f"{args.config}: {synth.CONFIGS[args.config]}",
+        "warmup": warmup, "ms_per_step": elapsed / steps * 1e3,
+        "config": {"workload": f"{config}: {synth.CONFIGS[config]}",
                    "micrographs_per_gpu": n_mg, "k": cfg.k, "box_size": cfg.box,
                    "boxes_per_gpu": N, "edges_per_gpu": E, "cliques_per_gpu": C,
                    "parallelism": f"dp{world} (micrograph shards)",
-                   "io": "host buffers over PCIe (--host-io)" if args.host_io else "HBM-resident",
+                   "io": "host buffers over PCIe (--host-io)" if host_io else "HBM-resident",
                    "steps_in_flight": 2 if pipeline else 1},
         "edges_per_sec": tot_e * steps / elapsed,
         "totals": {"micrographs": tot_mg, "edges": tot_e, "cliques": tot_c},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
-                     # priced against HBM (no contraction: no MFMA roofline applies); the
-                     # limiter is derived from this build's committed PMC counters
+        "roofline": {"bound": derived_bound(rec, kind, dom_bytes, dom_ms,
+                                            "k_fused" if kind == "k_fused" else max(avg, key=avg.get)),
+                     "priced_against": "hbm (no contraction: no MFMA roofline applies)",
+                     "kernel": dom, "achieved": achieved,
+                     # the limiter (and bound) come from this build's committed PMC counters
                      "limiter": limiter,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": traffic_src,
@@ -473,14 +480,87 @@ def main():
                      "kernel_ms": {k_: round(v, 4) for k_, v in sorted(avg.items())}},
         "gen_s": t_gen,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    return out, cfg, mgs
+
+
+def by_config_entry(rep):
+    """The compact per-config record of the by_config key."""
+    r = rep["roofline"]
+    return {"value": rep["value"], "unit": rep["unit"], "ms_per_step": rep["ms_per_step"],
+            "kernel_ms": r["kernel_ms_per_step"], "kernel": r["kernel"],
+            "steps": rep["steps"], "warmup": rep["warmup"],
+            "micrographs_per_gpu": rep["config"]["micrographs_per_gpu"],
+            "edges_per_sec": rep["edges_per_sec"], "totals": rep["totals"],
+            "roofline": {"frac": r["frac"], "achieved": r["achieved"], "bound": r["bound"],
+                         "traffic": r["traffic"], "traffic_source": r["traffic_source"],
+                         "hbm_frac_measured": r["hbm_frac_measured"], "limiter": r["limiter"],
+                         "alg_bytes_per_step": r["alg_bytes_per_step"]},
+            "kernel_ms_by_name": rep["pipeline"]["kernel_ms"]}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--n_mg", type=int, default=None, help="micrographs per GPU")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--host-io", action="store_true",
+                    help="PCIe-inclusive variant (never the headline value): host x/y/score and "
+                         "offsets are uploaded and every per-clique output is copied back to "
+                         "pinned host memory inside each step")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="synchronous rgc_run per step instead of two contexts in flight")
+    ap.add_argument("--by-config", default=None,
+                    help="comma-separated configs also timed in this run and reported under "
+                         "by_config (default: every other BASELINE config at its bench size, "
+                         "when --n_mg is not given; 'none' to skip)")
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
+    args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.launch_check:   # test hook: the launcher's rank layout, no GPU work
+        print(json.dumps({k_: os.environ.get(k_) for k_ in
+                          ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR")}), flush=True)
+        return
+
+    env = Env(args)
+    n_mg = args.n_mg or DEFAULT_MG[args.config]
+    rep, cfg, mgs = measure(args, env, args.config, n_mg, args.steps, args.warmup,
+                            host_io=args.host_io, no_pipeline=args.no_pipeline)
+    out = {"metric": "micrographs/sec (get_cliques, whole node) at 1/2/4/8 MI355X; % HBM roofline"}
+    out.update(rep)
+    out.update({"higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "dtype": "f64", "data": "synthetic (seeded SURVEY.md §8(d) generator)"})
+    # the other BASELINE configs in the same run (same steps / warmup, their bench sizes:
+    # C4 at the 100k / 8-GPU shard of 12.5k micrographs per GPU); the CPU baseline stays on
+    # the headline config
+    if args.by_config is None:
+        extra = [] if args.n_mg else [c for c in ("C2", "C3", "C4", "C5") if c != args.config]
+    elif args.by_config.lower() == "none":
+        extra = []
+    else:
+        extra = [c.strip() for c in args.by_config.split(",") if c.strip()]
+    if extra and not args.host_io:
+        byc = {args.config: by_config_entry(rep)}
+        for c in extra:
+            r_c, _, _ = measure(args, env, c, DEFAULT_MG[c], args.steps, args.warmup,
+                                no_pipeline=args.no_pipeline)
+            byc[c] = by_config_entry(r_c)
+        out["by_config"] = byc
+    if env.rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, mgs, args.cpu_budget, config=args.config)
-    if rank == 0:
+    if env.rank == 0:
         print(json.dumps(out), flush=True)
-    for c in ctxs:
-        c.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    if env.dist is not None:
+        env.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -21,6 +21,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cfloat>
 #include <cstring>
 #include <cstdint>
 #include <fcntl.h>
@@ -79,6 +80,10 @@ locale_t c_locale() {
 }
 
 // Exact powers of ten 10^0 .. 10^27 in x87 extended precision (5^27 < 2^64: every one is exact)
+// fast_decimal reads the 64-bit significand of the quotient from the low 8 bytes of the long
+// double: only valid for the x87 80-bit format (a 64-bit or IEEE-quad long double would misparse)
+static_assert(LDBL_MANT_DIG == 64 && sizeof(long double) >= 10,
+              "box_parse.cpp's fast decimal path needs x87 80-bit long double");
 struct Pow10L {
   long double v[28];
   Pow10L() {

@@ -1542,7 +1542,12 @@ int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) 
   A.cs = D<double>(c, D_IL_CS);
   A.count = D<unsigned int>(c, D_IL_CNT);
   TRY(mark(c, "k_ilp_cert"));
+  HIPCHK(hipMemsetAsync(A.count, 0, 16, s));
   rgc::launch_ilp_cert(s, 0, A);
+  // no component left unproven by the branch and bound (the common case): nothing to certify
+  HIPCHK(hipMemcpyAsync(H<int64_t>(c, H_TOTAL) + 3, A.count, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const bool any_flagged = reinterpret_cast<uint32_t*>(H<int64_t>(c, H_TOTAL) + 3)[1] != 0;
   // rounds until a pass changes nothing (each round settles at least the heaviest undecided
   // clique / makes at least one improving swap, so both terminate); counters read every 4
   auto rounds = [&](int phase, int cap) -> int {
@@ -1555,14 +1560,16 @@ int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) 
     }
     return 0;
   };
-  TRY(rounds(1, 1 << 20));
-  TRY(rounds(2, 1 << 16));
-  rgc::launch_ilp_cert(s, 3, A);
-  // projected subgradient iterations of the Lagrangian bound (per component Polyak steps
-  // towards the primal; after 20 iterations without progress the step halves and lam
-  // restarts from the best one)
-  for (int it = 0; it < 1000; ++it) rgc::launch_ilp_cert(s, 4, A);
-  rgc::launch_ilp_cert(s, 5, A);
+  if (any_flagged) {
+    TRY(rounds(1, 1 << 20));
+    TRY(rounds(2, 1 << 16));
+    rgc::launch_ilp_cert(s, 3, A);
+    // projected subgradient iterations of the Lagrangian bound (per component Polyak steps
+    // towards the primal; after 20 iterations without progress the step halves and lam
+    // restarts from the best one)
+    for (int it = 0; it < 1000; ++it) rgc::launch_ilp_cert(s, 4, A);
+    rgc::launch_ilp_cert(s, 5, A);
+  }
   TRY(mark(c, "d2h_x"));
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(x, A.x, nc, hipMemcpyDeviceToHost, s));

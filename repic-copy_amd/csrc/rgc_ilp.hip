@@ -499,6 +499,7 @@ __global__ __launch_bounds__(ILP_WG) void k_cert_flag(IlpArgs A) {
   if (n > ILP_BIG) f = 2;
   else if (n > 1 && A.exact[A.members[A.comp_off[comp]]] == 0) f = 1;
   A.cert[comp] = f;
+  if (f) atomicAdd(A.count + 1, 1u);   // flagged components (the host skips the rest when 0)
   double* cs = A.cs + comp * CS;
   cs[0] = 0.0; cs[1] = 0.0; cs[2] = INFINITY; cs[3] = 2.0; cs[4] = 0.0; cs[5] = 0.0; cs[6] = 0.0;
   cs[7] = 0.0;

@@ -354,21 +354,27 @@ class _Run:
         q = queue.Queue(maxsize=2)
         stop = threading.Event()
 
+        def put(item):
+            """Queue ``item`` unless the consumer has stopped (it raised, or is done): every
+            put, the end sentinel and a parser exception included, gives up once ``stop`` is
+            set, so the join below cannot wait on a full queue nobody reads."""
+            while not stop.is_set():
+                try:
+                    q.put(item, timeout=0.1)
+                    return True
+                except queue.Full:
+                    continue
+            return False
+
         def produce():
             try:
                 for ch in self.plan_chunks():
-                    while not stop.is_set():
-                        try:
-                            q.put(ch, timeout=0.1)
-                            break
-                        except queue.Full:
-                            continue
-                    if stop.is_set():
+                    if not put(ch):
                         return
             except BaseException as e:  # noqa: BLE001 - re-raised by the consumer
-                q.put(e)
+                put(e)
                 return
-            q.put(None)
+            put(None)
 
         th = threading.Thread(target=produce, name="rgc-parse", daemon=True)
         th.start()

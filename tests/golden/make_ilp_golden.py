@@ -5,7 +5,8 @@ gap 0) on the same models.  The large ones (C3 micrographs, C5 windows with comp
 >10k cliques) take seconds to minutes of CPU per solve on the GPU box, so their optima are
 computed once here and committed: ``ilp_highs.npz`` maps a sha256 of each model (shape, COO
 rows/cols, f32 weights) to the HiGHS objective and its packing (chosen column indices).
-``tests/test_ilp.py:highs`` falls back to a live solve for a model that is not in the file.
+``tests/test_ilp.py:highs`` fails for a model that is not in the file (no live solves on the
+GPU box).
 
     python tests/golden/make_ilp_golden.py
 """

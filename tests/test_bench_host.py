@@ -44,3 +44,17 @@ def test_c5_cpu_baseline_is_sampled_and_bounded():
     assert time.perf_counter() - t0 < 10
     assert cb["cores"] == 1 and cb["kind"] == "port" and 0 < cb["value"] < 0.1
     assert "extrapolated" in cb["sample"] and "upper bound" in cb["sample"]
+
+
+def test_roofline_bound_follows_the_counters():
+    """roofline.bound is derived from the same counters as the limiter, never a literal."""
+    valu = {"kernels": {"k_fused": {"traffic": 243e6, "derived": {"valu_busy": 0.9}}}}
+    assert bench.derived_bound(valu, "k_fused", 995e6, 0.48) == "valu"
+    lat = {"kernels": {"k_fused": {"traffic": 2.4e9, "derived": {"valu_busy": 0.54}}}}
+    assert bench.derived_bound(lat, "k_fused", 7.5e9, 3.4) == "latency"
+    hbm = {"kernels": {"k_fused": {"traffic": 4.4e9, "derived": {"valu_busy": 0.3}}}}
+    assert bench.derived_bound(hbm, "k_fused", 4e9, 1.0) == "hbm"
+    assert bench.derived_bound(None, "k_fused", 1.0, 1.0) == "unmeasured"
+    assert bench.derived_bound({"step_traffic": 2e9}, "route", 8e9, 8.0, "k5l") == "unmeasured"
+    route = {"step_traffic": 2e9, "kernels": {"k5_epilogue": {"derived": {"valu_busy": 0.7}}}}
+    assert bench.derived_bound(route, "route", 8e9, 8.0, "k5_epilogue") == "valu"

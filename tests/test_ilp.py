@@ -20,17 +20,28 @@ from golden_util import load_case
 _HIGHS = None
 
 
+# largest model tests/test_ilp.py:highs may solve live (10017 micrographs: <= ~600 cliques)
+LIVE_MAX_COLS = 2000
+
+
 def highs(A, w):
-    """HiGHS optimum (x uint8, objective) of the model: from tests/golden/ilp_highs.npz
-    (make_ilp_golden.py, keyed by the model's sha256) when present, else a live solve."""
+    """HiGHS optimum (x uint8, objective) of the model from tests/golden/ilp_highs.npz
+    (make_ilp_golden.py, keyed by the model's sha256).  Only small models (at most
+    LIVE_MAX_COLS cliques: milliseconds of HiGHS) may be solved live when missing; a larger one
+    missing from the fixture fails the test at once, since a GPU test must never wait minutes
+    on a CPU MILP (regenerate the fixture with tests/golden/make_ilp_golden.py instead)."""
     global _HIGHS
     import make_ilp_golden
-    from oracle import ilp_ref
     if _HIGHS is None:
         _HIGHS = make_ilp_golden.load()
     hit = _HIGHS.get(make_ilp_golden.model_key(A, w))
     if hit is None:
-        return ilp_ref.milp(A, w)
+        if A.shape[1] <= LIVE_MAX_COLS:
+            from oracle import ilp_ref
+            return ilp_ref.milp(A, w)
+        raise AssertionError(f"ILP model with {A.shape[1]} cliques not in "
+                             "tests/golden/ilp_highs.npz: run tests/golden/make_ilp_golden.py "
+                             "to add its HiGHS optimum")
     x = np.zeros(A.shape[1], np.uint8)
     x[hit[1]] = 1
     return x, hit[0]

@@ -21,7 +21,7 @@ n_mg = int(sys.argv[2]) if len(sys.argv) > 2 else 10000
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 7
 cfg = synth.SynthConfig(**synth.CONFIGS[cfg_name], seed=0)
 batch = Batch.pack(cfg.k, cfg.box, synth.batch(cfg, n_mg))
-libs = sorted(glob.glob(os.path.join(ROOT, "repic-copy_amd/repic_amd/ablate/*.so"))) + [_lib.LIB_PATH]
+libs = sorted(glob.glob(os.path.join(ROOT, "abl/*.so"))) + [_lib.LIB_PATH]
 if len(sys.argv) > 4:   # one library only (per-phase PMC passes: tools/gpu_pmc_ablate.sh)
     libs = [sys.argv[4]]
 

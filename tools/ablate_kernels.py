@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-kernel device times (median over interleaved rounds) of every library under
-repic_amd/ablate/ and the product build on one synthetic batch.
+abl/ and the product build on one synthetic batch.
 
   python tools/ablate_kernels.py C5 16 7
 """
@@ -21,7 +21,7 @@ n_mg = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 7
 cfg = synth.SynthConfig(**synth.CONFIGS[cfg_name], seed=0)
 batch = Batch.pack(cfg.k, cfg.box, synth.batch(cfg, n_mg))
-libs = sorted(glob.glob(os.path.join(ROOT, "repic-copy_amd/repic_amd/ablate/*.so"))) + [_lib.LIB_PATH]
+libs = sorted(glob.glob(os.path.join(ROOT, "abl/*.so"))) + [_lib.LIB_PATH]
 
 
 class Runner:

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Timing-only GPU pass: every library under repic_amd/ablate/ plus the product build, timed
+# Timing-only GPU pass: every library under abl/ plus the product build, timed
 # interleaved in one process (tools/ablate.py).  No parity tests: experiments only.
 #   gpurun --timeout 300 -- bash tools/gpu_ab.sh TAG [CONFIG] [N_MG]
 set -e -o pipefail

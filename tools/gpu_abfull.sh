@@ -1,6 +1,6 @@
 #!/bin/bash
 # Full GPU parity suite on the product build, then interleaved A/B timing of every library
-# under repic_amd/ablate/ + the product build on C2, C4 and C3.  First failure ends the script.
+# under abl/ + the product build on C2, C4 and C3.  First failure ends the script.
 #   gpurun --timeout 900 -- bash tools/gpu_abfull.sh TAG
 set -e -o pipefail
 TAG=${1:-abfull}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B pass: selected parity tests on the product build, then interleaved timing of every
-# library under repic_amd/ablate/ + the product build on C2 and C4.
+# library under abl/ + the product build on C2 and C4.
 #   gpurun --timeout 600 -- bash tools/gpu_abtest.sh TAG "pytest -k expr"
 set -e -o pipefail
 TAG=${1:-abtest}; KEXPR=${2:-}

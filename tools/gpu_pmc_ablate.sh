@@ -1,14 +1,17 @@
 #!/bin/bash
 # Per-phase PMC attribution: each ablation build (fused kernel stops after phase N) and the
 # product build run under one SQ counter pass; marginal counts per phase = differences.
-#   make -C repic-copy_amd/csrc ablate && gpurun --timeout 900 -- bash tools/gpu_pmc_ablate.sh TAG [C2] [n_mg]
+#   make -C repic-copy_amd/csrc ablate && gpurun --timeout 900 -- bash tools/gpu_pmc_ablate.sh TAG [C2] [n_mg] [COUNTERS]
+# COUNTERS (one pass, <= 8 SQ counters): default the issue/stall set; "lane" = VALU lane
+# efficiency per phase (SQ_ACTIVE_INST_VALU, SQ_THREAD_CYCLES_VALU, SQ_INSTS_VALU)
 set -e -o pipefail
 TAG=${1:-pmcabl}; CFG=${2:-C2}; NMG=${3:-10000}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-CNT="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH"
-for L in repic-copy_amd/repic_amd/ablate/librepic_gc_stop*.so repic-copy_amd/repic_amd/librepic_gc.so; do
+CNT=${4:-"SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH"}
+[ "$CNT" = lane ] && CNT="SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES"
+for L in abl/librepic_gc_stop*.so repic-copy_amd/repic_amd/librepic_gc.so; do
   b=$(basename "$L" .so)
   timeout -s KILL 120 rocprofv3 --pmc $CNT --output-format csv -d "$OUT/$b" -o run -- \
     python3 tools/ablate.py "$CFG" "$NMG" 1 "$L" > "$OUT/$b.txt" 2> "$OUT/$b.err" || { tail -20 "$OUT/$b.err"; exit 1; }

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Timing-only experiment pass: tools/ablate.py on each CONFIG (every library under
-# repic_amd/ablate/ plus the product build, interleaved in one process), then once more per
+# abl/ plus the product build, interleaved in one process), then once more per
 # RGC_DIAG_NT value (workgroup size forced for every library).  No parity tests.
 #   gpurun --timeout 600 -- bash tools/gpu_xp.sh TAG "C2 C4" "256"
 set -e -o pipefail
