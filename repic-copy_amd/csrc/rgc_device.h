@@ -12,6 +12,38 @@ namespace rgc {
 constexpr int WG = 256;
 constexpr int NW = WG / 64;
 
+// A kernel argument as its own scalar value.  The kernel-argument lowering loads neighbouring
+// FusedArgs fields with one s_load_dwordx16; kept live across the kernel, such a 16-SGPR tuple
+// is spilled to VGPR lanes as a unit, and every later use of ONE of its fields reloaded all 16
+// lanes (v_readlane: VALU issue slots) - 74 per clique in P6.  An s_mov through asm copies the
+// field out of the tuple once (a new value the coalescer cannot fold back into the tuple), so
+// a spill of it costs one or two lanes.  Pointers come back as global (address space 1)
+// pointers, so their accesses stay global_load / global_store.
+template <typename T>
+using gptr = __attribute__((address_space(1))) T*;
+template <typename T>
+__device__ __forceinline__ gptr<T> gdetach(T* p) {
+  uint64_t v = (uint64_t)p, r;
+  asm volatile("s_mov_b64 %0, %1" : "=s"(r) : "s"(v));
+  return (gptr<T>)(T*)r;
+}
+__device__ __forceinline__ double sdetach(double v) {
+  double r;
+  asm volatile("s_mov_b64 %0, %1" : "=s"(r) : "s"(v));
+  return r;
+}
+__device__ __forceinline__ int sdetach(int v) {
+  int r;
+  asm volatile("s_mov_b32 %0, %1" : "=s"(r) : "s"(v));
+  return r;
+}
+__device__ __forceinline__ int64_t sdetach(int64_t v) {
+  int64_t r;
+  asm volatile("s_mov_b64 %0, %1" : "=s"(r) : "s"(v));
+  return r;
+}
+
+
 // ----------------------------------------------------------------------------- block reductions
 template <int BS = WG>
 __device__ __forceinline__ double block_min(double v, double* lds) {

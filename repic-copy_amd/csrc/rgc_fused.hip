@@ -55,7 +55,10 @@ struct FusedHdr {
   int E, nodes, cc_cnt, cc_max, target, V, status;
   uint32_t ccur;    // P4 clique-queue cursor
   int tief[2];      // P6: some clique of the chunk needs the order pass (by chunk parity)
-  int qslot;        // QG: the workgroup's HBM level-tree slot (-1: none, LDS queue)
+  union {
+    int qslot;      // QG (K = 4): the workgroup's HBM level-tree slot (-1: none, LDS queue)
+    int trifail;    // K = 3: the triangle pass overflowed (p4_tri)
+  };
   int64_t C, base;
 };
 
@@ -134,13 +137,13 @@ struct FCtx {
   double B, two_b2;
   float Bf, two_b2f;   // (float) copies, wave-uniform (SGPRs)
   int flags;
-  const double* score;
-  int32_t* rows;
-  float* w;
-  float* conf;
-  int32_t* consensus;
-  int32_t* members;
-  uint8_t* order;
+  gptr<const double> score;
+  gptr<int32_t> rows;
+  gptr<float> w;
+  gptr<float> conf;
+  gptr<int32_t> consensus;
+  gptr<int32_t> members;
+  gptr<uint8_t> order;
   FShared S;
   int pb[K + 1];     // picker bounds (local box indices)
   int pp[K + 1];     // picker bounds (sorted positions; pp[K] = first non-finite box)
@@ -153,8 +156,8 @@ struct FCtx {
   uint16_t* cq_ord;  // P4 queue: ordinal of each queued clique within its root's DFS
   uint32_t* ccur;    // P4 queue cursor (LDS)
   int cq_cap;        // P4 queue capacity (cliques)
-  int32_t* tie_list;              // set-order ties for k_fused_ties
-  unsigned long long* tie_count;
+  gptr<int32_t> tie_list;         // set-order ties for k_fused_ties
+  gptr<unsigned long long> tie_count;
   int64_t tie_cap;
 };
 
@@ -494,9 +497,9 @@ __device__ __forceinline__ void fused_epilogue_order(const FCtx<K>& c, int64_t j
     if (c.set_order) {
       // CPython set order (64-bit tuple hashing and set probing): appended for k_fused_ties,
       // which keeps that code out of this kernel's registers (ties: ~0.6 % of C2's cliques)
-      const unsigned long long t = atomicAdd(c.tie_count, 1ull);
+      const unsigned long long t = atomicAdd((unsigned long long*)c.tie_count, 1ull);
       if ((int64_t)t < c.tie_cap) {
-        int32_t* e = c.tie_list + (int64_t)t * (4 + K);
+        gptr<int32_t> e = c.tie_list + (int64_t)t * (4 + K);
         e[0] = (int32_t)(uint32_t)(uint64_t)j;
         e[1] = (int32_t)(uint32_t)((uint64_t)j >> 32);
         e[2] = c.m;
@@ -778,6 +781,93 @@ __device__ __forceinline__ BfsOut<K> bfs_cliques(const FShared& S, FusedHdr& H, 
   }
 }
 
+// ----------------------------------------------------------------------------- P4 (K = 3)
+// Triangles r < h < t (one box per picker, pairwise adjacent; get_cliques.py:49-56,160-161)
+// in ONE pass, thread per root r (picker-0 position): for each picker-1 neighbour h of r (the
+// first segment [fwd[r], split[r]) of r's sorted list), merge h's sorted forward list (all
+// picker 2) with r's picker-2 segment [split[r], fwd[r+1]); every common t is a triangle.  The
+// first TRI_CACHE triangles of a root stay in registers; a wave reserves the queue slots of
+// all its roots with one LDS atomic (wave prefix sum of the counts), so no workgroup barrier
+// or level tree sits between the roots and their cliques.  Slot records are 8 bytes: (r | h <<
+// 16, t | ordinal << 16), the ordinal being the triangle's rank in its root's lexicographic
+// order, so the output index (root's scanned offset + ordinal) does not depend on the slot.
+// Per-root counts go to cnt[r] for that scan.  Returns false when the queue region or the
+// 15-bit ordinals overflow (the caller then runs the BFS).
+constexpr int TRI_CACHE = 3;
+
+template <int NT>
+__device__ __forceinline__ bool p4_tri(const FShared& S, FusedHdr& H, char* q, int qbytes, int n0,
+                                       bool get_cc, uint32_t target, int tid) {
+  const uint32_t cap = (uint32_t)(qbytes / 8);
+  uint2* rec = reinterpret_cast<uint2*>(q);
+  bool over = false;
+  for (int r0 = 0; r0 < n0; r0 += NT) {   // (uniform trip count: the wave ops below)
+    const int r = r0 + tid;
+    uint32_t cnt = 0, c0 = 0, c1 = 0, c2 = 0;
+    const bool ok = r < n0 && S.fwd[r] < S.fwd[r + 1] && (!get_cc || S.parent[r] == target);
+    int lo1 = 0, hi1 = 0, lo2 = 0, hi2 = 0;
+    if (ok) {
+      lo1 = S.fwd[r];
+      hi1 = S.split[r];
+      lo2 = hi1;
+      hi2 = S.fwd[r + 1];
+    }
+    // walk: fn(h, t) for every triangle of root r, in lexicographic order
+    auto walk = [&](auto&& fn) {
+      for (int e = lo1; e < hi1; ++e) {
+        const int h = S.dst[e];
+        int i = S.fwd[h];
+        const int ie = S.fwd[h + 1];
+        int j = lo2;
+        while (i < ie && j < hi2) {
+          const int a = S.dst[i], b = S.dst[j];
+          if (a == b) fn(h, a);
+          i += a <= b ? 1 : 0;
+          j += b <= a ? 1 : 0;
+        }
+      }
+    };
+    if (lo2 < hi2) {
+      walk([&](int h, int t) {
+        const uint32_t pk = (uint32_t)h | ((uint32_t)t << 16);
+        c0 = cnt == 0 ? pk : c0;
+        c1 = cnt == 1 ? pk : c1;
+        c2 = cnt == 2 ? pk : c2;
+        ++cnt;
+      });
+    }
+    if (r < n0) S.cnt[r] = cnt;
+    // slots for the wave's roots: one LDS atomic per wave
+    const int inc = wave_incl_add32((int)cnt);
+    uint32_t base = 0;
+    if ((tid & 63) == 63 && inc > 0) base = atomicAdd(&H.ccur, (uint32_t)inc);
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, 63);
+    const uint32_t s0 = base + (uint32_t)(inc - (int)cnt);
+    over |= cnt > 0x7FFFu || s0 + cnt > cap;
+    if (cnt == 0 || s0 + cnt > cap || cnt > 0x7FFFu) continue;
+    auto put = [&](uint32_t o, uint32_t pk) {
+      rec[s0 + o] = make_uint2((uint32_t)r | (pk << 16), (pk >> 16) | (o << 16));
+      S.flags[pk & 0xFFFF] = 3;
+      S.flags[pk >> 16] = 3;
+    };
+    S.flags[r] = 3;
+    put(0, c0);
+    if (cnt > 1) put(1, c1);
+    if (cnt > 2) put(2, c2);
+    if (cnt > TRI_CACHE) {   // rare: the rest by a second walk
+      uint32_t o = 0;
+      walk([&](int h, int t) {
+        if (o >= TRI_CACHE) put(o, (uint32_t)h | ((uint32_t)t << 16));
+        ++o;
+      });
+    }
+  }
+  // any thread's overflow fails the whole micrograph's triangle pass (trifail: 0 since P1)
+  if (over) H.trifail = 1;
+  __syncthreads();
+  return H.trifail == 0;
+}
+
 // Candidates of a box: the 2x3 cell stencil at its cell in the grid of every HIGHER picker
 // (forward edges only): columns cx, cx + 1 from cx = its column - 1 or its column (by the
 // half of the column the box lies in), rows y0..y1, i.e. up to 2 (K - 1 - p) ranges of
@@ -901,7 +991,7 @@ __device__ __forceinline__ int pairs_count(const Stencil& st, const FShared& S, 
 template <int K>
 __device__ __forceinline__ int pairs_count_int(const Stencil& st, const FShared& S,
                                                const GridU& H, float Bf, float Tf,
-                                               uint32_t* mask_out) {
+                                               uint32_t* mask_out, int ts = 0) {
   uint32_t mask = 0, pk = 0;
   int cnt = 0, kk = 0;
   const float ax = (float)st.a.x, ay = (float)st.a.y;
@@ -947,10 +1037,17 @@ __device__ __forceinline__ int pairs_count_int(const Stencil& st, const FShared&
           ++cnt;
           mask |= (kk < 32) ? (1u << kk) : 0u;
           pk = (pk << 16) | (uint32_t)t;
+#ifdef RGC_X_CNTUNION   // experiment: the CC unions in the count pass
+          S.flags[t] = 1;
+          uf_union_lds(S.parent, (uint32_t)ts, (uint32_t)t);
+#endif
         }
       }
     }
   }
+#ifdef RGC_X_CNTUNION
+  if (cnt) S.flags[ts] = 1;
+#endif
 #endif
   *mask_out = cnt <= 2 ? pk : mask;
   return cnt;
@@ -1006,6 +1103,8 @@ __device__ __forceinline__ void put_stats(const FusedArgs& A, int m, int status,
   A.o.clique_cnt[m] = C;
   if (status == 0 || status == RGC_ST_NO_CLIQUES || status == RGC_ST_NO_EDGES)
     atomicAdd(A.cursor + 1, (unsigned long long)edges);
+  else   // needs another pass: counted, so a run's totals alone tell the host (lazy stats)
+    atomicAdd(A.cursor + 4, 1ull);
 }
 
 // Waves per SIMD the register allocator targets.  K = 3 fits 64 VGPRs (4 small spills) for 8
@@ -1067,7 +1166,7 @@ void k_fused(FusedArgs A) {
   S.cbuf = reinterpret_cast<uint16_t*>(smem + L.off_cbuf);
   const int tid = threadIdx.x;
   const int m = A.mg_list ? A.mg_list[blockIdx.x] : (int)blockIdx.x;
-  if (blockIdx.x == 0 && tid < 4 && A.cursor_clear) A.cursor_clear[tid] = 0;   // next run's
+  if (blockIdx.x == 0 && tid < 8 && A.cursor_clear) A.cursor_clear[tid] = 0;   // next run's
 #ifdef RGC_STAMPS
   // diagnostic build only: per-phase s_memtime stamps of thread 0 (never in the product .so)
 #define STAMP(i)                                                                            \
@@ -1096,12 +1195,17 @@ void k_fused(FusedArgs A) {
 #endif
   STAMP(0);
   FCtx<K> c;
-  c.B = A.B; c.two_b2 = A.two_b2; c.flags = A.flags; c.score = A.score;
+  c.B = sdetach(A.B); c.two_b2 = sdetach(A.two_b2); c.flags = sdetach(A.flags);
+  c.score = gdetach(A.score);
   c.Bf = uff((float)A.B);
   c.two_b2f = uff((float)A.two_b2);
-  c.rows = A.rows; c.w = A.w; c.conf = A.conf; c.consensus = A.consensus;
-  c.members = A.members; c.order = A.order;
-  c.tie_list = A.tie_list; c.tie_count = A.cursor + 3; c.tie_cap = A.tie_cap;
+  c.rows = gdetach(A.rows); c.w = gdetach(A.w); c.conf = gdetach(A.conf);
+  c.consensus = gdetach(A.consensus);
+  c.members = gdetach(A.members); c.order = gdetach(A.order);
+  c.tie_list = gdetach(A.tie_list); c.tie_count = gdetach(A.cursor) + 3;
+  c.tie_cap = sdetach(A.tie_cap);
+  const gptr<const double> ax = gdetach(A.x);
+  const gptr<const double> ay = gdetach(A.y);
   c.S = S;
   c.m = m;
   c.b0 = A.box_off[m * K];
@@ -1118,8 +1222,8 @@ void k_fused(FusedArgs A) {
 #pragma unroll
   for (int j = 0; j < RB; ++j) {
     const int i = tid + j * FWG;
-    rx[j] = i < n ? A.x[b0 + i] : 0.0;
-    ry[j] = i < n ? A.y[b0 + i] : 0.0;
+    rx[j] = i < n ? ax[b0 + i] : 0.0;
+    ry[j] = i < n ? ay[b0 + i] : 0.0;
   }
   // fn(i, x, y) for every box of this thread
   auto each_box = [&](auto&& fn) {
@@ -1128,7 +1232,7 @@ void k_fused(FusedArgs A) {
       const int i = tid + j * FWG;
       if (i < n) fn(i, rx[j], ry[j]);
     }
-    for (int i = tid + RB * FWG; i < n; i += FWG) fn(i, A.x[b0 + i], A.y[b0 + i]);
+    for (int i = tid + RB * FWG; i < n; i += FWG) fn(i, ax[b0 + i], ay[b0 + i]);
   };
   // bounding box on floats for the f32 layout (exact there; a micrograph with inexact
   // coordinates is deferred to the f64 layout, where it is computed in f64)
@@ -1148,7 +1252,6 @@ void k_fused(FusedArgs A) {
     }
   });
   if (inexact) bmnx = -INFINITY;   // (impossible otherwise) carried through the min reduction
-  double mnx, mny, mxx, mxy;
   // P1's packed bucket counters (the whole cell-start region of the size class), union-find
   // parents, node flags and P2's packed CC-size counters are set up here, so the bounding-box
   // barrier orders them too
@@ -1173,21 +1276,7 @@ void k_fused(FusedArgs A) {
     if ((tid & 63) == 63)
 #pragma unroll
       for (int r = 0; r < 4; ++r) H.red4[r][tid >> 6] = (double)bv[r];
-    double v[4];
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      v[r] = H.red4[r][0];
-#pragma unroll
-      for (int w = 1; w < FNW; ++w) v[r] = fmin(v[r], H.red4[r][w]);
-    }
-    mnx = v[0]; mny = v[1]; mxx = -v[2]; mxy = -v[3];
   }
-  if (!W && mnx == -INFINITY) {   // needs the f64 layout: the host relaunches it wide
-    if (tid == 0) put_stats(A, m, RGC_ST_DEFER_WIDE, 0, 0, 0, 0, 0, 0, 0);
-    return;
-  }
-
   STOP_AFTER(0);
   STAMP(1);
   // ---- P1: one grid per picker (x-major cells, K * gx * gy <= 4 nmax + 4 cells in all) and
@@ -1197,15 +1286,22 @@ void k_fused(FusedArgs A) {
   // box's half of its column (its x is within 0.4986 columns), three rows around its row: a
   // 2x3 stencil, i.e. two contiguous position ranges per grid.  Per-picker grids let a box
   // visit the boxes of higher pickers only.
-  // the grid is planned by every thread from the reduced bounding box (identical values, no
-  // thread-0 section and barrier); thread 0 only records what later phases read.  Planned in
-  // f32 with hardware reciprocals (every wave pays for it): exactness is not needed, only
-  // cells >= 1.08 B x 0.54 B (0.28 % above what an edge needs, far above f32 rounding; the
-  // half-column test has 0.0014 columns of slack), K gx gy within the budget (checked on the
-  // integers used), and one inv_cell / inv_celly used by every key.
-  GridU G;
-  double xbs;
-  {
+  // Wave 0 alone reduces the per-wave bounding boxes and plans the grid (wave-uniform work:
+  // done by every wave it cost ~8x its VALU); the other waves read the plan from the header
+  // after one barrier.  Planned in f32 with hardware reciprocals: exactness is not needed,
+  // only cells >= 1.08 B x 0.54 B (0.28 % above what an edge needs, far above f32 rounding;
+  // the half-column test has 0.0014 columns of slack), K gx gy within the budget (checked on
+  // the integers used), and one inv_cell / inv_celly used by every key.
+  __syncthreads();
+  if (tid < 64) {
+    double v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v[r] = H.red4[r][0];
+#pragma unroll
+      for (int w = 1; w < FNW; ++w) v[r] = fmin(v[r], H.red4[r][w]);
+    }
+    const double mnx = v[0], mny = v[1], mxx = -v[2], mxy = -v[3];
     double cl = A.B, icl = 0.0, icly = 0.0;
     int gx = 0, gy = 0;
     if (mnx <= mxx && A.B > 0.0) {
@@ -1236,21 +1332,28 @@ void k_fused(FusedArgs A) {
         if (icly * (0.54 * A.B) > 1.0) icly = 1.0 / (0.54 * A.B);
       }
     }
-    G.minx = ufd(mnx); G.miny = ufd(mny); G.inv_cell = ufd(icl); G.inv_celly = ufd(icly);
-    G.inv_cellf = uff((float)icl);
-    G.gx = ufl(gx); G.gy = ufl(gy); G.ncell = G.gx * G.gy; G.nkey = K * G.ncell;
-    G.inv_gy = G.gy > 0 ? __builtin_amdgcn_rcpf((float)G.gy) : 0.0f;
-    const double ex = mxx - mnx;
-    xbs = ufd((mnx < mxx && ex < 0x1p60) ? (double)((float)n * __builtin_amdgcn_rcpf((float)ex))
-                                         : 0.0);
     if (tid == 0) {
+      const double ex = mxx - mnx;
       H.minx = mnx; H.miny = mny; H.cell = cl; H.inv_cell = icl; H.inv_celly = icly;
-      H.gx = G.gx; H.gy = G.gy;
-      H.ncell = G.ncell; H.nkey = G.nkey; H.inv_gy = G.inv_gy; H.xbs = xbs;
-      H.status = 0; H.C = 0; H.base = 0; H.V = 0; H.target = -1; H.ccur = 0;
+      H.gx = gx; H.gy = gy;
+      H.ncell = gx * gy; H.nkey = K * gx * gy;
+      H.inv_gy = gy > 0 ? __builtin_amdgcn_rcpf((float)gy) : 0.0f;
+      H.xbs = (mnx < mxx && ex < 0x1p60) ? (double)((float)n * __builtin_amdgcn_rcpf((float)ex))
+                                         : 0.0;
+      // -inf minimum: some coordinate is not an integer below 2^23 (P0), the host relaunches
+      // the micrograph with the f64 layout
+      H.status = (!W && mnx == -INFINITY) ? RGC_ST_DEFER_WIDE : 0;
+      H.C = 0; H.base = 0; H.V = 0; H.target = -1; H.ccur = 0;
       H.tief[0] = H.tief[1] = 0;
+      H.qslot = 0;   // (= trifail)
     }
   }
+  __syncthreads();
+  if (!W && H.status == RGC_ST_DEFER_WIDE) {
+    if (tid == 0) put_stats(A, m, RGC_ST_DEFER_WIDE, 0, 0, 0, 0, 0, 0, 0);
+    return;
+  }
+  const GridU G = grid_u(H);
   const int nk = G.nkey;
   // counting sort by key with packed u16 counters (two keys per LDS word, zeroed in P0).
   // Counts go to slot key + 1, so the exclusive scan leaves bucket q's start in slot q + 1;
@@ -1323,7 +1426,7 @@ void k_fused(FusedArgs A) {
     stencil_setup<K, W>(st, ts, S, G);
     uint32_t mask;
     int ec;
-    if constexpr (!W) ec = pairs_count_int<K>(st, S, G, (float)B, (float)ti, &mask);
+    if constexpr (!W) ec = pairs_count_int<K>(st, S, G, (float)B, (float)ti, &mask, ts);
     else ec = pairs_count<K, W>(st, S, G, B, two_b2, i_lo, i_hi, &mask);
     S.fwd[ts] = (uint16_t)ec;
     S.cnt[ts] = mask;
@@ -1350,6 +1453,11 @@ void k_fused(FusedArgs A) {
 #else
     const bool src_ok = 2 * E <= A.ecap;
 #endif
+#ifdef RGC_X_CNTUNION   // (integer layout: unions already done by the count)
+    constexpr bool cnt_union = !W;
+#else
+    constexpr bool cnt_union = false;
+#endif
     uint16_t* esrc = S.dst + E;
     for (int r0 = 0, odd = 0; r0 < n; r0 += FWG, odd ^= 1) {   // same order as the count
       const int ts = odd ? r0 + FWG - 1 - tid : r0 + tid;
@@ -1368,7 +1476,8 @@ void k_fused(FusedArgs A) {
         pairs_fill<K, W>(st, S, G, cw0, d, cnt, B, two_b2, i_lo, i_hi);
       }
       S.flags[i] = 1;
-      if (src_ok) {
+      if (cnt_union) {
+      } else if (src_ok) {
         for (int e = 0; e < cnt; ++e) esrc[base + e] = (uint16_t)i;
       } else {
         for (int e = 0; e < cnt; ++e) {
@@ -1380,7 +1489,7 @@ void k_fused(FusedArgs A) {
     __syncthreads();
     STAMP(5);   // fill
     STOP_AFTER(23);
-    if (src_ok) {
+    if (src_ok && !cnt_union) {
       for (int e = tid; e < E; e += FWG) {
         const uint32_t h = S.dst[e];
         S.flags[h] = 1;
@@ -1529,7 +1638,20 @@ void k_fused(FusedArgs A) {
   BfsOut<K> bo;
   int nch = 0;
   int64_t C = 0;
-  {
+  // K = 3: one-pass triangle listing into the LDS queue (p4_tri); the BFS below only when its
+  // queue overflowed
+  bool tri = false;
+  if constexpr (K == 3) {
+#ifndef RGC_X_NOTRI
+    tri = p4_tri<NT>(S, H, q, qbytes, n0, get_cc, (uint32_t)target, tid);
+#endif
+    if (tri) {
+      C = block_scan_dpp<FWG>(S.cnt, n0, H.red64);   // root offsets (output order)
+      nch = 1;
+      bo.C = C;
+    }
+  }
+  if (!tri) {
     int r0 = 0, len = n0;
     bool ok = maxch >= 1;
     if (tid == 0) { chtab[0] = 0; chtab[1] = 0; }
@@ -1555,7 +1677,9 @@ void k_fused(FusedArgs A) {
     if (!ok) { nch = 0; C = 0; bo.C = -1; }
   }
   const bool bfs_ok = nch > 0;
-  if (bfs_ok) {
+  if (tri) {
+    c.cq_cap = (int)max(C, (int64_t)1);   // slot records in q (P6 reads them)
+  } else if (bfs_ok) {
     // cliques = level-K tree entries (members by walking parents); their flag words follow
     c.cq_cap = (int)max(bo.C, (int64_t)1);
     c.cq_ord = reinterpret_cast<uint16_t*>(q + bo.lvl[K] + 4 * (int)bo.C);
@@ -1641,8 +1765,10 @@ void k_fused(FusedArgs A) {
       blist[bcnt[xbucket(ld(t).x)] + S.vrank[t]] = (uint16_t)t;
     }
     __syncthreads();
-    for (int t = tid; t < n; t += FWG) {
-      if (S.flags[t] != 3) continue;
+    // ranks over the dense bucket-ordered vertex list (every lane holds a vertex; the
+    // position loop above skips the non-vertices)
+    for (int u0 = tid; u0 < V; u0 += FWG) {
+      const int t = blist[u0];
       const int vi = S.citems[t];
       const CT2 v = ld(t);
       const int b = xbucket(v.x);
@@ -1690,7 +1816,10 @@ void k_fused(FusedArgs A) {
     for (int ci = 0; ci < nit; ++ci) {
       int c0, c1;
       if (tid == 0) H.tief[(ci + 1) & 1] = 0;   // last read before the previous chunk's end
-      if (bfs_ok) {
+      if (tri) {
+        c0 = 0;
+        c1 = Cm;
+      } else if (bfs_ok) {
         const int ch = ci == 0 ? nch - 1 : ci - 1;
         c0 = ufl((int)chtab[2 * ch + 1]);
         c1 = ufl((int)chtab[2 * ch + 3]);
@@ -1718,8 +1847,17 @@ void k_fused(FusedArgs A) {
         }
         __syncthreads();
       }
-      // members of chunk slot sl: BFS tree walk, or the re-walk buffer
-      auto clique_members = [&](int sl, int (&mem)[K]) {
+      // members of chunk slot sl: triangle record, BFS tree walk, or the re-walk buffer; the
+      // output index of the slot; the order-pass flag of the slot
+      uint2* trec = reinterpret_cast<uint2*>(q);
+      auto clique_members = [&](int sl, int (&mem)[K]) -> int64_t {
+        if (tri) {
+          const uint2 rr = trec[sl];
+          mem[0] = (int)(rr.x & 0xFFFF);
+          mem[1] = (int)(rr.x >> 16);
+          mem[K - 1] = (int)(rr.y & 0xFFFF);
+          return obase + (int64_t)(S.cnt[mem[0]] + ((rr.y >> 16) & 0x7FFF));
+        }
         if (bfs_ok) {
           BfsLevel<K, K, NT>::prefix(q, cur.lvl, (uint32_t)sl, mem);
         } else {
@@ -1727,20 +1865,29 @@ void k_fused(FusedArgs A) {
 #pragma unroll
           for (int i = 0; i < K; ++i) mem[i] = sb[i];
         }
+        return obase + (c0 + sl);
+      };
+      auto set_order_flag = [&](int sl) {
+        if (tri) reinterpret_cast<uint32_t*>(trec)[2 * sl + 1] |= 0x80000000u;
+        else c.cq_ord[sl] |= 0x8000;
+      };
+      auto order_flag = [&](int sl) -> bool {
+        if (tri) return (trec[sl].y & 0x80000000u) != 0;
+        return (c.cq_ord[sl] & 0x8000) != 0;
       };
       bool any = false;
       for (int sl = tid; sl < c1 - c0; sl += FWG) {
         int mem[K];
-        clique_members(sl, mem);
+        const int64_t jo = clique_members(sl, mem);
 #ifdef RGC_X_NOEPI   // timing experiment only: members walked, no epilogue
         if (mem[0] == 0xFFFFF) c.cq_ord[sl] = 1;
         continue;
 #endif
         bool order;
-        if constexpr (!W) order = fused_epilogue_main<K, W, true>(c, obase + (c0 + sl), mem);
-        else order = fused_epilogue_main<K, W, false>(c, obase + (c0 + sl), mem);
+        if constexpr (!W) order = fused_epilogue_main<K, W, true>(c, jo, mem);
+        else order = fused_epilogue_main<K, W, false>(c, jo, mem);
         if (order) {
-          c.cq_ord[sl] |= 0x8000;
+          set_order_flag(sl);
           any = true;
         }
       }
@@ -1752,11 +1899,10 @@ void k_fused(FusedArgs A) {
       if (H.tief[ci & 1]) {
 #endif
         for (int sl = tid; sl < c1 - c0; sl += FWG) {
-          const uint32_t o = c.cq_ord[sl];
-          if (!(o & 0x8000)) continue;
+          if (!order_flag(sl)) continue;
           int mem[K];
-          clique_members(sl, mem);
-          fused_epilogue_order<K, W>(c, obase + (c0 + sl), mem);
+          const int64_t jo = clique_members(sl, mem);
+          fused_epilogue_order<K, W>(c, jo, mem);
         }
       }
       __syncthreads();

@@ -293,6 +293,7 @@ __device__ __forceinline__ void wave_sync() {
 // lanes holding that box drop out, until none is left - the sequential greedy's result.
 __global__ __launch_bounds__(64) void k_ilp_wave(IlpArgs A, int n_big) {
   __shared__ uint64_t open[ILP_BIG * 8 / 64];
+  __shared__ uint64_t mark[ILP_BIG * 8 / 64];   // rows of the candidates (Lagrangian bound)
   __shared__ uint16_t lrs[ILP_LRCAP];
   __shared__ int counter;
   const int lane = threadIdx.x;
@@ -312,6 +313,10 @@ __global__ __launch_bounds__(64) void k_ilp_wave(IlpArgs A, int n_big) {
     double* wl = reinterpret_cast<double*>(stk + (int64_t)n * (W + 2));   // n
     int32_t* tmpid = reinterpret_cast<int32_t*>(wl + n);          // K n
     uint16_t* lrg = reinterpret_cast<uint16_t*>(tmpid + (int64_t)K * n);   // (K + 1) n
+    // Lagrangian bound data (components with pre-B&B multipliers, cert == 3): multiplier of
+    // each local row, max(0, reduced weight) of each member
+    double* lamloc = reinterpret_cast<double*>(base + A.wlag_off);          // K n
+    double* posw = lamloc + (int64_t)K * n;                                 // n
     int32_t* sorted = reinterpret_cast<int32_t*>(stk);
     for (int i = lane; i < n; i += 64) {
       int r = 0;
@@ -348,8 +353,55 @@ __global__ __launch_bounds__(64) void k_ilp_wave(IlpArgs A, int n_big) {
     if (lds_rows)
       for (int t = lane; t < n * (K + 1); t += 64) lrs[t] = lrg[t];
     const uint16_t* lr = lds_rows ? lrs : lrg;
+    // Lagrangian relaxation of the box constraints with the component's multipliers lam >= 0
+    // (projected subgradient before the search, rgc_ilp_solve): for any candidate set P,
+    //   max packing of P <= sum over rows r of P of lam_r + sum over i in P of max(0, w_i - sum
+    //   over i's rows of lam_r),
+    // near the LP optimum when lam is, so it prunes where the greedy clique cover cannot (the
+    // crowded C3 components' integrality gaps are 0.03-0.8 %).  Used as min(cover, lagrangian)
+    const bool lag = A.cert != nullptr && A.lam != nullptr && A.cert[comp] == 3;
+    if (lag) {
+      for (int i = lane; i < n; i += 64) {
+        const int32_t c = m[i];
+        const int64_t e0 = A.col_ptr[c], e1 = A.col_ptr[c + 1];
+        double rc = wl[i];
+        for (int64_t e = e0; e < e1; ++e) {
+          const double l = A.lam[A.row_idx[e]];
+          rc -= l;
+          lamloc[lr[i * (K + 1) + (int)(e - e0)]] = l;
+        }
+        posw[i] = rc > 0.0 ? rc : 0.0;
+      }
+    }
     wave_sync();
     const int ow = (nrow + 63) / 64;
+    // the Lagrangian bound of candidate set P (all lanes get the wave's sum), padded by a
+    // relative 1e-12 so its f64 rounding can never prune a better packing
+    auto lag_bound = [&](uint64_t P) {
+      for (int q = lane; q < ow; q += 64) mark[q] = 0;
+      __builtin_amdgcn_wave_barrier();
+      double s = 0.0;
+      for (int q = 0; q < W; ++q) {
+        const uint64_t word = __shfl(P, q, 64);
+        if (!((word >> lane) & 1)) continue;
+        const int i = q * 64 + lane;
+        s += posw[i];
+        const uint16_t* li = lr + i * (K + 1);
+        for (int a = 0; a < K; ++a)
+          atomicOr(reinterpret_cast<unsigned long long*>(mark) + (li[a] >> 6), 1ull << (li[a] & 63));
+      }
+      __builtin_amdgcn_wave_barrier();
+      for (int q = lane; q < ow; q += 64) {
+        uint64_t wd = mark[q];
+        while (wd) {
+          s += lamloc[q * 64 + __builtin_ctzll(wd)];
+          wd &= wd - 1;
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      return s * (1.0 + 1e-12);
+    };
     auto bound = [&](uint64_t P) {
       for (int q = lane; q < ow; q += 64) open[q] = 0;
       __builtin_amdgcn_wave_barrier();
@@ -405,7 +457,7 @@ __global__ __launch_bounds__(64) void k_ilp_wave(IlpArgs A, int n_big) {
       if (nz == 0) {
         if (cur > best) { best = cur; best_set = chosen; }
         back = true;
-      } else if (cur + bound(P) <= best) {
+      } else if ((lag && cur + lag_bound(P) <= best) || cur + bound(P) <= best) {
         back = true;
       } else {
         const int fl = __builtin_ctzll(nz);
@@ -505,6 +557,28 @@ __global__ __launch_bounds__(ILP_WG) void k_cert_flag(IlpArgs A) {
   cs[7] = 0.0;
 }
 
+// before the wave search: components of 65..ILP_BIG cliques get multipliers for the search's
+// Lagrangian bound (cert 3: greedy primal, swaps, subgradient, like the certification below)
+__global__ __launch_bounds__(ILP_WG) void k_cert_flag_pre(IlpArgs A) {
+  const int64_t comp = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (comp >= A.n_comp) return;
+  const int n = A.comp_n[comp];
+  const uint8_t f = (n > ILP_SMALL && n <= ILP_BIG) ? 3 : 0;
+  A.cert[comp] = f;
+  if (f) atomicAdd(A.count + 1, 1u);
+  double* cs = A.cs + comp * CS;
+  cs[0] = 0.0; cs[1] = 0.0; cs[2] = INFINITY; cs[3] = 2.0; cs[4] = 0.0; cs[5] = 0.0; cs[6] = 0.0;
+  cs[7] = 0.0;
+}
+// after the pre-search subgradient: the best multipliers (kept in rmax) become lam
+__global__ __launch_bounds__(ILP_WG) void k_lr_take_best(IlpArgs A) {
+  const int64_t r = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (r >= A.n_rows) return;
+  const int64_t comp = ilp_row_comp(A, r);
+  if (comp < 0 || A.cert[comp] == 0) return;
+  A.lam[r] = reinterpret_cast<const double*>(A.rmax)[r];
+}
+
 // per column: priority key and state; chosen columns of node-limit components own their rows
 __global__ __launch_bounds__(ILP_WG) void k_cert_cols(IlpArgs A) {
   const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
@@ -513,7 +587,7 @@ __global__ __launch_bounds__(ILP_WG) void k_cert_cols(IlpArgs A) {
   const double w = A.w[c];
   A.key[c] = ((uint64_t)__float_as_uint((float)fmax(w, 0.0)) << 32) | (uint32_t)~(uint32_t)c;
   uint8_t st = ST_NONE;
-  if (f == 2) st = w > 0.0 ? ST_UND : ST_OUT;
+  if (f == 2 || f == 3) st = w > 0.0 ? ST_UND : ST_OUT;
   else if (f == 1) st = A.x[c] ? ST_IN : ST_OUT;
   A.st[c] = st;
   if (st == ST_IN)
@@ -703,6 +777,8 @@ __global__ __launch_bounds__(ILP_WG) void k_cert_final(IlpArgs A) {
   const double P = cs[4], Lb = cs[2];
   const bool ok = Lb - P <= 1e-4 * fabs(P);
   A.exact[c] = ok ? RGC_ILP_GAP_OK : (A.cert[comp] == 2 ? RGC_ILP_HEURISTIC : RGC_ILP_NODE_LIMIT);
+  // the component's absolute gap, once (at its first column), for micrograph-level MIPGap
+  if (A.gap && c == A.members[A.comp_off[comp]]) A.gap[c] = fmax(Lb - P, 0.0);
 }
 // (before k_lr_init: the primal value is recounted from the final packing)
 __global__ __launch_bounds__(ILP_WG) void k_cert_reset_primal(IlpArgs A) {
@@ -746,6 +822,14 @@ void launch_ilp_cert(hipStream_t stream, int phase, const IlpArgs& A) {
       break;
     case 5:
       RGC_L(k_cert_final, nbc);
+      break;
+    case 6:   // pre-search setup (cert 3) = phase 0 with k_cert_flag_pre
+      RGC_L(k_cert_flag_pre, nbk);
+      if (nbr) RGC_L(k_cert_rows_init, nbr);
+      RGC_L(k_cert_cols, nbc);
+      break;
+    case 7:
+      if (nbr) RGC_L(k_lr_take_best, nbr);
       break;
   }
 #undef RGC_L

@@ -22,14 +22,21 @@ inline hipError_t set_dyn_lds_once(std::atomic<uint64_t>& done, const void* fn, 
 }
 
 constexpr int MAX_K = 8;            // largest picker count with a compiled clique kernel
-constexpr int CELL_CAP = 8192;      // LDS counters per micrograph grid (k1_bin)
 constexpr int SCAN_TILE = 2048;     // elements per scan workgroup
 
-// Uniform grid of one micrograph: cells of side `cell` (>= box_size) over its bounding box.
+// Per-picker grids of one micrograph (k1_bin): gx x gy cells per picker, columns `cell` =
+// 1 / inv_cell wide (>= 1.08 B), rows >= 0.54 B tall, keys picker * ncell + cx * gy + cy;
+// nkey = k * ncell (non-finite boxes); flags bit 0: integer layout (exact f32 JI test).
 struct MgGrid {
-  double minx, miny, cell;
-  int gx, gy, ncell, pad;
+  double minx, miny, cell, inv_cell, inv_celly;
+  int gx, gy, ncell, nkey, flags, pad;
 };
+// cell-start entries of a micrograph of n boxes (k1_bin): its key budget + 2; wide = the u32
+// counter variant (some micrograph of the batch has more than 65535 boxes)
+__host__ __device__ inline int bin_budget(int64_t n, bool wide) {
+  const int64_t cap = wide ? 32760 : 65528;
+  return (int)(2 * n + 64 < cap ? 2 * n + 64 : cap);
+}
 
 // Per-micrograph results.
 struct MgStat {
@@ -187,7 +194,7 @@ struct CliqueArgs {
 void launch_bin(hipStream_t stream, int n_mg, int k, double B, const int32_t* box_off,
                 const int32_t* cell_off, const double* x, const double* y, MgGrid* grid,
                 int32_t* cell_start, double* sx, double* sy, int32_t* sbox, uint8_t* spick,
-                int32_t* smg, int32_t* bmg, uint8_t* bpick);
+                int32_t* smg, int32_t* bmg, uint8_t* bpick, bool wide, int max_n);
 void launch_pairs(hipStream_t stream, bool fill, int N, int k, double B, double two_b2,
                   const int32_t* box_off, const int32_t* cell_off, const MgGrid* grid,
                   const int32_t* cell_start, const double* sx, const double* sy,
@@ -269,6 +276,7 @@ struct IlpArgs {
   unsigned int* n_big;
   uint64_t* wscratch;         // wave solver: wstride words per wave
   int64_t wstride;
+  int64_t wlag_off;           // wave solver: offset (words) of the Lagrangian-bound arrays
   uint8_t* x;                 // [n_cols] solution
   uint8_t* exact;             // [n_cols] RGC_ILP_* status of the column's component
   // certification stage (components not proven optimal by the branch and bound)
@@ -281,12 +289,14 @@ struct IlpArgs {
   double* grad;               // [n_rows] subgradient (cover count in between)
   double* cs;                 // [n_comp * 8] per component: lsum g2 lbest mu primal step stall
   unsigned int* count;        // round counter
+  double* gap;                // optional [n_cols]: component bound - packing at its first column
 };
 int ilp_small_max();
 int ilp_big_max();
 void launch_ilp(hipStream_t stream, int phase, const IlpArgs& A, int n_big, int n_waves);
 // certification stage (rgc_ilp.hip): phase 0 setup, 1 greedy round, 2 swap round, 3 primal
-// and multiplier init, 4 subgradient iteration, 5 final statuses
+// and multiplier init, 4 subgradient iteration, 5 final statuses; 6 pre-search setup of the
+// wave components' multipliers (cert 3), 7 best multipliers -> lam
 void launch_ilp_cert(hipStream_t stream, int phase, const IlpArgs& A);
 
 }  // namespace rgc

@@ -26,103 +26,162 @@
 
 namespace rgc {
 
-__device__ __forceinline__ int cell_of(const MgGrid& G, double x, double y) {
-  if (G.ncell == 0 || !isfinite(x) || !isfinite(y)) return G.ncell;  // overflow bucket
-  int cx = (int)fmin(floor((x - G.minx) / G.cell), (double)(G.gx - 1));
-  int cy = (int)fmin(floor((y - G.miny) / G.cell), (double)(G.gy - 1));
-  return cy * G.gx + cx;
+// ----------------------------------------------------------------------------- K1 bin
+// Per-picker grids (the fused kernel's P1 restated for whole-GPU kernels): every picker gets
+// its own gx x gy grid of cells >= 1.08 B wide and >= 0.54 B tall over the micrograph's
+// bounding box, keys picker * ncell + (cx * gy + cy) (x-major), the non-finite boxes in key
+// nkey = K * ncell.  JI > 0.3 needs I > (6/13) B^2, i.e. |dx|, |dy| < (7/13) B = 0.5385 B, so
+// an edge partner lies within 0.4986 columns: in the box's own column or the neighbouring
+// one on the side of the box's half of its column, and within one row: a 2 x 3 stencil = two
+// contiguous position ranges per higher picker's grid (forward edges only).  Keys and the
+// half test use the same f64 product (x - minx) * inv_cell for every box, so the plan is
+// consistent (0.0014 columns of slack against rounding).
+__device__ __forceinline__ int bin_key(const MgGrid& G, int p, double x, double y) {
+  if (G.ncell == 0 || !isfinite(x) || !isfinite(y)) return G.nkey;
+  const int cx = (int)fmin(floor((x - G.minx) * G.inv_cell), (double)(G.gx - 1));
+  const int cy = (int)fmin(floor((y - G.miny) * G.inv_celly), (double)(G.gy - 1));
+  return p * G.ncell + cx * G.gy + cy;
 }
 
-// ----------------------------------------------------------------------------- K1 bin
-// One workgroup per micrograph: bounding box, grid choice (cell = box_size, doubled until
-// the grid fits the micrograph's cell budget), LDS counting sort of its boxes by cell.
-__global__ __launch_bounds__(WG) void k1_bin(int k, double B, const int32_t* __restrict__ box_off,
-                                             const int32_t* __restrict__ cell_off,
-                                             const double* __restrict__ x,
-                                             const double* __restrict__ y, MgGrid* grid,
-                                             int32_t* cell_start, double* sx, double* sy,
-                                             int32_t* sbox, uint8_t* spick, int32_t* smg,
-                                             int32_t* bmg, uint8_t* bpick) {
-  __shared__ int32_t cnt[CELL_CAP];
-  __shared__ double redd[NW];
-  __shared__ int64_t red64[NW];
+// One workgroup per micrograph: bounding box, grid plan, integer-layout flag (every finite
+// coordinate an integer below 2^23 and an integer 1 <= B <= 2896: P2's exact f32 test),
+// LDS counting sort of the boxes by key.  cell_start[cell_off[m] + key] = first sorted
+// position (local to the micrograph) of each key; entry nkey + 1 = n.
+template <bool WIDE>
+__global__ __launch_bounds__(1024) void k1_bin(int k, double B, const int32_t* __restrict__ box_off,
+                                               const int32_t* __restrict__ cell_off,
+                                               const double* __restrict__ x,
+                                               const double* __restrict__ y, MgGrid* grid,
+                                               int32_t* cell_start, double* sx, double* sy,
+                                               int32_t* sbox, uint8_t* spick, int32_t* smg,
+                                               int32_t* bmg, uint8_t* bpick) {
+  constexpr int BT = 1024, BW = BT / 64;
+  extern __shared__ __attribute__((aligned(16))) uint32_t cntw[];   // packed counters
+  __shared__ double redd[BW];
+  __shared__ int64_t red64[BW];
   __shared__ int32_t poff[MAX_K + 1];
+  __shared__ int notint;
   __shared__ MgGrid G;
   const int m = blockIdx.x;
   const int b0 = box_off[m * k], b1 = box_off[m * k + k], n = b1 - b0;
-  if ((int)threadIdx.x <= k) poff[threadIdx.x] = box_off[m * k + threadIdx.x];
+  if ((int)threadIdx.x <= k) poff[threadIdx.x] = box_off[m * k + threadIdx.x] - b0;
+  if (threadIdx.x == 0) notint = !(B >= 1.0 && B <= 2896.0 && B == floor(B));
   double mnx = INFINITY, mny = INFINITY, mxx = -INFINITY, mxy = -INFINITY;
-  for (int i = threadIdx.x; i < n; i += WG) {
+  bool ni = false;
+  for (int i = threadIdx.x; i < n; i += BT) {
     const double xv = x[b0 + i], yv = y[b0 + i];
     if (isfinite(xv) && isfinite(yv)) {
       mnx = fmin(mnx, xv); mxx = fmax(mxx, xv);
       mny = fmin(mny, yv); mxy = fmax(mxy, yv);
+      ni |= xv != rint(xv) || yv != rint(yv) || fabs(xv) >= 0x1p23 || fabs(yv) >= 0x1p23;
     }
   }
-  mnx = block_min(mnx, redd);
-  mny = block_min(mny, redd);
-  mxx = block_max(mxx, redd);
-  mxy = block_max(mxy, redd);
+  __syncthreads();
+  if (ni) notint = 1;
+  mnx = block_min<BT>(mnx, redd);
+  mny = block_min<BT>(mny, redd);
+  mxx = block_max<BT>(mxx, redd);
+  mxy = block_max<BT>(mxy, redd);
+  const int budget = bin_budget(n, WIDE);
   if (threadIdx.x == 0) {
     MgGrid g;
-    g.minx = mnx; g.miny = mny; g.cell = B; g.gx = 0; g.gy = 0; g.ncell = 0; g.pad = 0;
-    const int budget = min(n + 1, CELL_CAP - 1);
+    g.minx = mnx; g.miny = mny; g.cell = INFINITY; g.inv_cell = 0.0; g.inv_celly = 0.0;
+    g.gx = 0; g.gy = 0; g.ncell = 0; g.nkey = 0; g.flags = notint ? 0 : 1;
     if (mnx <= mxx && B > 0.0) {
       const double ex = mxx - mnx, ey = mxy - mny;
       if (!(ex < 0x1p40 && ey < 0x1p40)) {
-        // coordinates beyond the exactness range of the stencil argument: one cell, all pairs
-        g.cell = INFINITY; g.gx = 1; g.gy = 1;
+        // beyond the exactness range of the stencil argument: one cell per picker, all pairs
+        g.gx = 1; g.gy = 1;
       } else {
-        double c = B;
+        // row height h, column width 2 h (>= 1.08 B x 0.54 B), k gx gy <= budget
+        const int per = budget / k;
+        double h = fmax(0.54 * B * (1.0 + 1e-9), fmax(sqrt(0.5 * ex * ey / per),
+                                                     fmax(0.5 * ex, ey) / per));
         for (;;) {
-          const double fx = floor(ex / c) + 1.0, fy = floor(ey / c) + 1.0;
-          if (fx * fy <= (double)budget) { g.gx = (int)fx; g.gy = (int)fy; break; }
-          c *= 2.0;
+          const double fx = floor(ex / (2.0 * h)) + 1.0, fy = floor(ey / h) + 1.0;
+          if (fx * fy <= (double)per) { g.gx = (int)fx; g.gy = (int)fy; break; }
+          h *= 1.0625;
         }
-        g.cell = c;
+        g.cell = 2.0 * h;
+        g.inv_cell = 1.0 / (2.0 * h);
+        g.inv_celly = 1.0 / h;
+        if (g.inv_cell * (1.08 * B) > 1.0) g.inv_cell = 1.0 / (1.08 * B);
+        if (g.inv_celly * (0.54 * B) > 1.0) g.inv_celly = 1.0 / (0.54 * B);
       }
       g.ncell = g.gx * g.gy;
+      g.nkey = k * g.ncell;
     }
     G = g;
     grid[m] = g;
   }
   __syncthreads();
-  const int nc = G.ncell;
-  for (int c = threadIdx.x; c <= nc; c += WG) cnt[c] = 0;
+  const int nk = G.nkey;   // keys 0..nk (nk: non-finite boxes)
+  const int nwords = WIDE ? nk + 2 : (nk + 3) / 2;
+  for (int c = threadIdx.x; c < nwords; c += BT) cntw[c] = 0;
   __syncthreads();
-  for (int i = threadIdx.x; i < n; i += WG) atomicAdd(&cnt[cell_of(G, x[b0 + i], y[b0 + i])], 1);
-  __syncthreads();
-  // exclusive scan of cnt[0..nc]
-  const int per = (nc + 1 + WG - 1) / WG;
-  const int c0 = min((int)threadIdx.x * per, nc + 1), c1 = min(c0 + per, nc + 1);
-  int64_t s = 0;
-  for (int c = c0; c < c1; ++c) s += cnt[c];
-  int64_t tot;
-  int64_t pre = block_excl_scan(s, red64, &tot);
-  int32_t* cs = cell_start + cell_off[m];
-  for (int c = c0; c < c1; ++c) {
-    const int v = cnt[c];
-    cnt[c] = (int)pre;
-    cs[c] = (int)pre;
-    pre += v;
+  auto picker = [&](int i) {
+    int p = 0;
+    for (int q = 1; q < k; ++q) p += i >= poff[q] ? 1 : 0;
+    return p;
+  };
+  for (int i = threadIdx.x; i < n; i += BT) {
+    const int q = bin_key(G, picker(i), x[b0 + i], y[b0 + i]);
+    if (WIDE) atomicAdd(&cntw[q], 1u);
+    else atomicAdd(&cntw[q >> 1], 1u << (16 * (q & 1)));
   }
-  if (threadIdx.x == 0) cs[nc + 1] = n;
   __syncthreads();
-  for (int i = threadIdx.x; i < n; i += WG) {
+  // exclusive scan of the nk + 1 counters into cell starts (LDS and cell_start)
+  auto cnt_at = [&](int c) -> uint32_t {
+    return WIDE ? cntw[c] : (cntw[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
+  };
+  const int per = (nk + 1 + BT - 1) / BT;
+  const int c0 = min((int)threadIdx.x * per, nk + 1), c1 = min(c0 + per, nk + 1);
+  int64_t s = 0;
+  for (int c = c0; c < c1; ++c) s += cnt_at(c);
+  int64_t tot;
+  int64_t pre = block_excl_scan<BT>(s, red64, &tot);
+  int32_t* cs = cell_start + cell_off[m];
+  for (int c = c0; c < c1; ++c) cs[c] = (int)pre, pre += cnt_at(c);
+  if (threadIdx.x == 0) cs[nk + 1] = n;
+  __syncthreads();   // every thread read its counters before they become cursors
+  // cursors = cell starts, in the counters' representation (u16 pairs: n <= 65535, so a
+  // cursor never carries into its neighbour)
+  for (int c = threadIdx.x; c < nwords; c += BT) {
+    if (WIDE) {
+      cntw[c] = c <= nk ? (uint32_t)cs[c] : 0u;
+    } else {
+      const int c0w = 2 * c, c1w = 2 * c + 1;
+      cntw[c] = (c0w <= nk ? (uint32_t)cs[c0w] : 0u) | ((c1w <= nk ? (uint32_t)cs[c1w] : 0u) << 16);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += BT) {
     const int g = b0 + i;
     const double xv = x[g], yv = y[g];
-    int p = 0;
-    while (p + 1 < k && g >= poff[p + 1]) ++p;
-    const int pos = b0 + atomicAdd(&cnt[cell_of(G, xv, yv)], 1);
+    const int p = picker(i);
+    const int q = bin_key(G, p, xv, yv);
+    int slot;
+    if (WIDE) {
+      slot = (int)atomicAdd(&cntw[q], 1u);
+    } else {
+      const int sh = 16 * (q & 1);
+      slot = (int)((atomicAdd(&cntw[q >> 1], 1u << sh) >> sh) & 0xFFFFu);
+    }
+    const int pos = b0 + slot;
     sx[pos] = xv; sy[pos] = yv; sbox[pos] = g; spick[pos] = (uint8_t)p; smg[pos] = m;
     bmg[g] = m; bpick[g] = (uint8_t)p;
   }
 }
 
 // ----------------------------------------------------------------------------- K2 pairs
-// One thread per box (in cell order, so neighbouring threads share stencil cells in L1/L2).
-// COUNT: forward-edge count per box.  FILL: write (target, JI) into the box's CSR slot and
-// sort it by target box index (picker-major, file order) for the clique intersections.
+// One thread per box (sorted position, so neighbouring threads share stencil cells in L1/L2):
+// the 2 x 3 stencil (see K1) in the grid of every HIGHER picker.  Integer micrographs decide
+// JI > 0.3 exactly on f32 (overlaps B - |dx| and their product < 2^24 are exact: I >
+// floor(6 B^2 / 13), the fused kernel's P2 test); others test I > (6/13) B^2 in f64 and
+// evaluate the reference quotient (get_cliques.py:40-46) only inside a 2^-40 relative band of
+// the threshold.  COUNT: forward-edge count per box.  FILL: write the targets (and, for the
+// RGC_F_EDGES hook only, the reference JI) into the box's CSR slot, sorted by target box index
+// (picker-major, file order) for the clique intersections.
 template <bool FILL>
 __global__ __launch_bounds__(WG) void k2_pairs(int N, int k, double B, double two_b2,
                                                const int32_t* __restrict__ box_off,
@@ -146,22 +205,47 @@ __global__ __launch_bounds__(WG) void k2_pairs(int N, int k, double B, double tw
   int cnt = 0;
   int64_t base = 0;
   if (FILL) base = fwd_off[g];
-  const int c = cell_of(G, xa, ya);
-  if (c < G.ncell) {
-    const int cx = c % G.gx, cy = c / G.gx;
+  const int key = bin_key(G, p, xa, ya);
+  if (key < G.nkey && p + 1 < k) {
+    const int cell = key - p * G.ncell;
+    const int cx = cell / G.gy, cy = cell - (cell / G.gy) * G.gy;
+    const double u = (xa - G.minx) * G.inv_cell;
+    const int sc = cx - ((u - (double)cx) < 0.5 ? 1 : 0);   // stencil columns sc, sc + 1
+    const int y0 = max(cy - 1, 0), y1 = min(cy + 1, G.gy - 1);
     const int b0 = box_off[m * k];
     const int32_t* cs = cell_start + cell_off[m];
-    const int xl = max(cx - 1, 0), xh = min(cx + 1, G.gx - 1);
-    for (int yy = max(cy - 1, 0); yy <= min(cy + 1, G.gy - 1); ++yy) {
-      const int lo = b0 + cs[yy * G.gx + xl], hi = b0 + cs[yy * G.gx + xh + 1];
-      for (int u = lo; u < hi; ++u) {
-        if (spick[u] <= p) continue;
-        const double xb = sx[u];
-        if (!(fabs(xa - xb) <= B)) continue;   // get_cliques.py:64
-        const double ji = jaccard(xa, ya, xb, sy[u], B, two_b2);
-        if (ji > 0.3) {                        // get_cliques.py:65 (threshold :138)
-          if (FILL) { e_dst[base + cnt] = sbox[u]; e_ji[base + cnt] = ji; }
-          ++cnt;
+    const bool intl = (G.flags & 1) != 0;
+    const float Bf = (float)B, Tf = (float)((6 * (int64_t)B * (int64_t)B) / 13);
+    const float axf = (float)xa, ayf = (float)ya;
+    const double t_star = 0.6 * B * B / 1.3;
+    const double i_lo = t_star * (1.0 - 0x1p-40), i_hi = t_star * (1.0 + 0x1p-40);
+    for (int q = p + 1; q < k; ++q) {
+      for (int d = 0; d <= 1; ++d) {
+        const int col = sc + d;
+        if (col < 0 || col >= G.gx) continue;
+        const int kb = q * G.ncell + col * G.gy;
+        const int lo = b0 + cs[kb + y0], hi = b0 + cs[kb + y1 + 1];
+        for (int v = lo; v < hi; ++v) {
+          const double xb = sx[v], yb = sy[v];
+          bool e;
+          if (intl) {
+            const float xo = fmaxf(Bf - fabsf(axf - (float)xb), 0.0f);
+            const float yo = fmaxf(Bf - fabsf(ayf - (float)yb), 0.0f);
+            e = xo * yo > Tf;
+          } else {
+            const double xo = fmax((fmin(xa, xb) + B) - fmax(xa, xb), 0.0);
+            const double yo = fmax((fmin(ya, yb) + B) - fmax(ya, yb), 0.0);
+            const double inter = xo * yo;
+            e = inter > i_hi;
+            if (!e && inter >= i_lo) e = inter / (two_b2 - inter) > 0.3;   // reference quotient
+          }
+          if (e) {
+            if (FILL) {
+              e_dst[base + cnt] = sbox[v];
+              if (e_ji) e_ji[base + cnt] = jaccard(xa, ya, xb, yb, B, two_b2);
+            }
+            ++cnt;
+          }
         }
       }
     }
@@ -169,17 +253,18 @@ __global__ __launch_bounds__(WG) void k2_pairs(int N, int k, double B, double tw
   if (!FILL) {
     fwd_cnt[g] = cnt;
   } else {
+    // insertion sort by target box (each picker's segment arrives in cell order)
     for (int i = 1; i < cnt; ++i) {
       const int kd = e_dst[base + i];
-      const double kj = e_ji[base + i];
+      const double kj = e_ji ? e_ji[base + i] : 0.0;
       int j = i - 1;
       while (j >= 0 && e_dst[base + j] > kd) {
         e_dst[base + j + 1] = e_dst[base + j];
-        e_ji[base + j + 1] = e_ji[base + j];
+        if (e_ji) e_ji[base + j + 1] = e_ji[base + j];
         --j;
       }
       e_dst[base + j + 1] = kd;
-      e_ji[base + j + 1] = kj;
+      if (e_ji) e_ji[base + j + 1] = kj;
     }
   }
 }
@@ -688,9 +773,23 @@ void launch_remap(hipStream_t stream, int64_t C, int k, const int32_t* orig, int
 void launch_bin(hipStream_t stream, int n_mg, int k, double B, const int32_t* box_off,
                 const int32_t* cell_off, const double* x, const double* y, MgGrid* grid,
                 int32_t* cell_start, double* sx, double* sy, int32_t* sbox, uint8_t* spick,
-                int32_t* smg, int32_t* bmg, uint8_t* bpick) {
-  RGC_LAUNCH(k1_bin, n_mg, WG, k, B, box_off, cell_off, x, y, grid, cell_start, sx, sy, sbox,
-             spick, smg, bmg, bpick);
+                int32_t* smg, int32_t* bmg, uint8_t* bpick, bool wide, int max_n) {
+  // (the caller passes wide = some micrograph of the batch has more than 65535 boxes, and
+  // the batch's largest micrograph: the counters of its key budget set the dynamic LDS)
+  if (n_mg <= 0) return;
+  const int keys = bin_budget(max_n, wide) + 2;
+  const int lds = (wide ? 4 * keys : 2 * (keys + 2)) + 16;
+  if (wide) {
+    static std::atomic<uint64_t> attr{0};
+    set_dyn_lds_once(attr, reinterpret_cast<const void*>(&k1_bin<true>), 132 * 1024);
+    hipLaunchKernelGGL(k1_bin<true>, dim3(n_mg), dim3(1024), lds, stream, k, B, box_off,
+                       cell_off, x, y, grid, cell_start, sx, sy, sbox, spick, smg, bmg, bpick);
+  } else {
+    static std::atomic<uint64_t> attr{0};
+    set_dyn_lds_once(attr, reinterpret_cast<const void*>(&k1_bin<false>), 132 * 1024);
+    hipLaunchKernelGGL(k1_bin<false>, dim3(n_mg), dim3(1024), lds, stream, k, B, box_off,
+                       cell_off, x, y, grid, cell_start, sx, sy, sbox, spick, smg, bmg, bpick);
+  }
 }
 
 void launch_pairs(hipStream_t stream, bool fill, int N, int k, double B, double two_b2,

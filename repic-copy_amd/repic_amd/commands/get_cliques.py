@@ -99,20 +99,22 @@ def _methods_after_reset(in_dir, out_dir):
 
 
 def _shard_weights(in_dir, methods, index, names):
-    """Per-micrograph pair-loop work estimate (sum over picker pairs of the product of the BOX
-    file sizes, a proxy for n_j * n_l) for balanced contiguous shards."""
-    w = np.empty(len(names))
-    for i, name in enumerate(names):
-        base = name.replace(".box", "")
-        sizes = []
-        for p, m in enumerate(methods):
-            fl = [name] if p == 0 else index.glob(m, f"*{base}*")
-            try:
-                sizes.append(sum(os.stat(os.path.join(in_dir, m, f)).st_size for f in fl))
-            except OSError:
-                sizes.append(0)
-        w[i] = 1.0 + pair_work(sizes)
-    return w
+    """Per-micrograph pair-loop work estimate for balanced contiguous shards (SURVEY.md
+    §8(e)): 1 + s^2 * k (k - 1) / 2 from the size s of the micrograph's picker-0 BOX file (a
+    proxy for sum over picker pairs of n_j * n_l, get_cliques.py:135-138).  One stat per
+    micrograph, from a thread pool (os.stat releases the GIL); no partner lookups."""
+    from concurrent.futures import ThreadPoolExecutor
+    d0 = os.path.join(in_dir, methods[0])
+
+    def size(name):
+        try:
+            return os.stat(os.path.join(d0, name)).st_size
+        except OSError:
+            return 0
+    with ThreadPoolExecutor(16) as ex:
+        s = np.fromiter(ex.map(size, names, chunksize=256), np.float64, len(names))
+    k = len(methods)
+    return 1.0 + s * s * (k * (k - 1) / 2.0)
 
 
 def _main(args, ctx, world, rank):
@@ -146,6 +148,9 @@ def _main(args, ctx, world, rank):
         b = shard_bounds(_shard_weights(args.in_dir, methods, index, names), world)
         lo, hi = b[rank], b[rank + 1]
     run = _Run(args, ctx, methods, index, names[lo:hi], lo)
+    # optimistic sharded writes need distinct output names: a failure's cleanup must never
+    # remove a file an earlier micrograph of another shard also wrote
+    run.unique_bases = len({n.replace(".box", "") for n in names}) == len(names)
     writer = None
     try:
         # large runs write from spawned processes, started now so they import during the
@@ -399,47 +404,83 @@ class _Run:
             th.join()
 
     def sharded(self, writer, dist, rank):
-        """One shard of a multi-rank run: plan every chunk (the shard's id offset needs all
-        lower shards' consumed ids), run the device, agree on the first failing micrograph,
-        then write up to it (no rank writes past a micrograph at which the reference raises)."""
+        """One shard of a multi-rank run.  The shard's global id offset needs every lower
+        shard's consumed ids, so the shard is parsed first (all ranks in parallel) and one
+        all-gather exchanges the counts; then chunks stream through the device with their
+        writes handed to the writer pool (device of chunk i+1 overlaps the writes of chunk i).
+        Writes are optimistic: a rank does not wait for the lower ranks' outcome.  The ranks
+        agree on the first failing micrograph at the end; files of micrographs at or after
+        it are removed again (the reference never wrote them), the rank owning it raises the
+        reference's exception, and every earlier micrograph's files exist."""
+        t_run = time.time()
+        spans = self.stats.setdefault("spans", [])
         chunks, err = [], None
         try:
             for ch in self.plan_chunks():
                 self.stats["parse_s"] += ch.parse_s
+                spans.append(("parse", ch.first, time.time() - ch.parse_s - t_run,
+                              time.time() - t_run))
                 chunks.append(ch)
         except Exception as e:  # noqa: BLE001 - re-raised by agree() after the exchange
             err = e
         consumed = chunks[-1].consumed if chunks else 0
         cons = agree(err, [consumed])
         id_off = sum(c[0] for c in cons[:rank])
-        fail = None
+        fail, stop_ch = None, None
+        optimistic = getattr(self, "unique_bases", True)
+        writer.spans, writer.t0 = spans, t_run
+        done = []
         try:
             for ch in chunks:
                 ch.shift_ids(id_off)
                 t0 = time.time()
                 self.device(ch)
                 ch.dev_s = time.time() - t0
+                spans.append(("device", ch.first, t0 - t_run, time.time() - t_run))
                 self.stats["chunks"] += 1
+                done.append(ch)
                 i = self.first_failure(ch)
-                if i is not None and fail is None:
+                if optimistic:
+                    self.write(ch, writer, i)        # up to its first failure (exclusive)
+                if i is not None:
                     fail = ch.first + i
+                    stop_ch = (ch, ch.mgs[i])
+                    break
         except Exception as e:  # noqa: BLE001
             err = e
         big = np.iinfo(np.int64).max
         rows = agree(err, [big if fail is None else fail])
         gfail = min(r_[0] for r_ in rows)
-        for ch in chunks:
-            if gfail != big and gfail < ch.first:
-                break                      # a lower rank's micrograph raises first
-            stop = None
-            if gfail != big and gfail < ch.first + len(ch.mgs):
-                stop = gfail - ch.first
-            self.write(ch, writer, stop)
-            if stop is not None:
-                if fail == gfail:          # this rank's own micrograph: earlier files, then raise
-                    writer.close()
-                    self.raise_for(ch.mgs[stop], ch)
-                break
+        if not optimistic:       # (duplicate output names) writes only up to the agreed failure
+            for ch in done:
+                if gfail < ch.first:
+                    break
+                self.write(ch, writer, gfail - ch.first if gfail < ch.first + len(ch.mgs)
+                           else None)
+        if gfail == big:
+            return
+        # a micrograph raises: every pending write lands first, then the files of the
+        # micrographs from the failing one on are removed (this shard's part of them)
+        writer.close()
+        if optimistic:
+            late = [mg.base for ch in done for i, mg in enumerate(ch.mgs)
+                    if ch.first + i >= gfail]
+            _remove_outputs(self.args.out_dir, late)
+        if fail == gfail:
+            self.raise_for(stop_ch[1], stop_ch[0])
+
+
+def _remove_outputs(out_dir, bases):
+    """Remove what the writers produce for these micrographs (get_cliques.py:123-130,
+    215-229): the empty <base>.box of a skip or the four pickles and the runtime line."""
+    for b in bases:
+        for suf in (".box", "_weight_vector.pickle", "_consensus_coords.pickle",
+                    "_consensus_confidences.pickle", "_constraint_matrix.pickle",
+                    "_runtime.tsv"):
+            try:
+                os.remove(os.path.join(out_dir, b + suf))
+            except FileNotFoundError:
+                pass
 
 
 class _FlatResult:

@@ -34,6 +34,9 @@ from ..ilp import solve_batch
 
 name = "run_ilp"
 
+STATUS_NAMES = {ilp.OPTIMAL: "OPTIMAL", ilp.GAP_OK: "GAP_OK", ilp.NODE_LIMIT: "NODE_LIMIT",
+                ilp.HEURISTIC: "HEURISTIC"}
+
 
 def add_arguments(parser):
     """Same CLI surface as the reference (run_ilp.py:16-23) plus tuning knobs."""
@@ -73,12 +76,12 @@ def main(args):
             break
         mats.append(A)
         weights.append(w)
-    xs, status = [], []
+    xs, status, rgap = [], [], []
     if mats:
         ctx = _lib.Context(dev)
         try:
-            xs, status = solve_batch(ctx, mats, weights, getattr(args, "node_limit", 0),
-                                     statuses=True)
+            xs, status, rgap = solve_batch(ctx, mats, weights, getattr(args, "node_limit", 0),
+                                           statuses=True, gaps=True)
         finally:
             ctx.close()
     share = (time.time() - t0) / max(1, len(mats))
@@ -119,6 +122,9 @@ def main(args):
                                         box_size, box_size, str(weight)]) + "\n")
         with open(out_file, "wt") as o:
             o.writelines(lines)
+        # run_ilp.py:132-136 appends the seconds; the certification status and the certified
+        # relative gap follow as two more columns, so an uncertified packing is visible
         with open(mf.replace("_constraint_matrix.pickle", "_runtime.tsv"), "a") as o:
-            o.write(str(share + time.time() - start) + "\n")
+            o.write(f"{share + time.time() - start}\t{STATUS_NAMES[status[i]]}\t"
+                    f"{rgap[i]:.3e}\n")
     sys.stdout.flush()

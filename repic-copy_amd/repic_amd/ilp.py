@@ -17,7 +17,7 @@ from . import _lib
 class IlpIn(C.Structure):
     _fields_ = [("n_cols", C.c_int64), ("n_rows", C.c_int64), ("col_ptr", C.c_void_p),
                 ("row_idx", C.c_void_p), ("w", C.c_void_p), ("node_limit", C.c_int64),
-                ("flags", C.c_uint32)]
+                ("flags", C.c_uint32), ("gap", C.c_void_p)]
 
 
 _lib.lib.rgc_ilp_solve.argtypes = [C.c_void_p, C.POINTER(IlpIn), C.c_void_p, C.c_void_p]
@@ -44,21 +44,27 @@ def pack(mats):
 NODE_LIMIT, OPTIMAL, GAP_OK, HEURISTIC = 0, 1, 2, 3
 
 
-def mg_status(ex):
-    """A micrograph's status from its columns' component statuses: the weakest one
-    (HEURISTIC < NODE_LIMIT < GAP_OK < OPTIMAL)."""
-    if len(ex) == 0:
+def mg_status(ex, gap=0.0, primal=0.0):
+    """A micrograph's status.  OPTIMAL when every conflict component was proven optimal;
+    else GAP_OK when the summed dual-bound gaps of its components are within 1e-4 of its
+    objective - the relative MIPGap at which Gurobi reports the micrograph's model optimal
+    (run_ilp.py:50-63 solves one model per micrograph, default parameters); else the weakest
+    component status (HEURISTIC < NODE_LIMIT)."""
+    if len(ex) == 0 or (ex == OPTIMAL).all():
         return OPTIMAL
-    for st in (HEURISTIC, NODE_LIMIT, GAP_OK):
+    if gap <= 1e-4 * abs(primal):
+        return GAP_OK
+    for st in (HEURISTIC, NODE_LIMIT):
         if (ex == st).any():
             return st
-    return OPTIMAL
+    return GAP_OK
 
 
-def solve_batch(ctx, mats, weights, node_limit=0, timing=False, statuses=False):
+def solve_batch(ctx, mats, weights, node_limit=0, timing=False, statuses=False, gaps=False):
     """Returns (x list of uint8 arrays, exact list of bool): per micrograph the chosen
     columns and whether every component was proven optimal (with ``statuses``: the
-    micrograph status codes, mg_status, instead of the bools)."""
+    micrograph status codes, mg_status, instead of the bools; with ``gaps`` also the
+    micrograph's relative gap bound, sum of component gaps / objective)."""
     col_ptr, row_idx, n_rows, col_off = pack(mats)
     w = np.ascontiguousarray(np.concatenate([np.asarray(v, np.float64).ravel() for v in weights])
                              if weights else np.zeros(0), dtype=np.float64)
@@ -68,11 +74,18 @@ def solve_batch(ctx, mats, weights, node_limit=0, timing=False, statuses=False):
         raise _lib.RGCError("batch too large for 32-bit row / column ids")
     x = np.zeros(nc, np.uint8)
     ex = np.zeros(nc, np.uint8)
+    gp = np.zeros(nc, np.float64)
     si = IlpIn(nc, n_rows, col_ptr.ctypes.data, row_idx.ctypes.data, w.ctypes.data,
-               int(node_limit), _lib.F_TIMING if timing else 0)
+               int(node_limit), _lib.F_TIMING if timing else 0, gp.ctypes.data)
     _lib._check(_lib.lib.rgc_ilp_solve(ctx._p, C.byref(si), x.ctypes.data, ex.ctypes.data))
     xs = [x[col_off[m]:col_off[m + 1]] for m in range(len(mats))]
-    st = [mg_status(ex[col_off[m]:col_off[m + 1]]) for m in range(len(mats))]
+    st, rel = [], []
+    for m in range(len(mats)):
+        a, b = col_off[m], col_off[m + 1]
+        primal = float(w[a:b][x[a:b] == 1].sum())
+        g = float(gp[a:b].sum())
+        st.append(mg_status(ex[a:b], g, primal))
+        rel.append(g / primal if primal > 0 else (0.0 if g == 0 else float("inf")))
     if statuses:
-        return xs, st
+        return (xs, st, rel) if gaps else (xs, st)
     return xs, [s_ == OPTIMAL for s_ in st]

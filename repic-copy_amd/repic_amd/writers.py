@@ -16,6 +16,7 @@ Python pickles them.
 from __future__ import annotations
 
 import os
+import time
 import pickle
 from concurrent.futures import ThreadPoolExecutor
 
@@ -269,6 +270,8 @@ class Writer:
         self._futs = []
         self._bases = set()
         self._items = []
+        # optional timeline: ("write", first base, submit, done) seconds after t0, per group
+        self.spans, self.t0 = None, 0.0
 
     def _submit(self, kind, args):
         base = args[1]
@@ -315,19 +318,28 @@ class Writer:
             self._drain()
         self._bases.update(names)
         args = (out_dir, items, w, conf, rows, cx, cy, cid)
+        t_sub = time.time()
         if self.native is not None and all(it[6] is None for it in items):
             if self._pool is None:
                 write_group_native(self.native, *args)
+                self._span(names, t_sub)
                 return
             self._futs.append(self._pool.submit(write_group_native, self.native, *args))
         elif self._pool is None:
             write_group(*args)
+            self._span(names, t_sub)
             return
         else:
             self._flush()
             self._futs.append(self._pool.submit(_write_chunk, [(2, args)]))
+        if self.spans is not None:
+            self._futs[-1].add_done_callback(lambda f, n=names, t=t_sub: self._span(n, t))
         if len(self._futs) > 4 * self.threads:
             self._drain(len(self._futs) // 2)
+
+    def _span(self, names, t_sub):
+        if self.spans is not None and names:
+            self.spans.append(("write", names[0], t_sub - self.t0, time.time() - self.t0))
 
     def close(self):
         try:

@@ -407,10 +407,13 @@ def _submit_wait_check():
     stream = torch.cuda.current_stream(dev).cuda_stream
     ctxs = [_lib.Context(0, stream), _lib.Context(0, stream)]
 
-    def submit(c, i):
+    def submit(c, i, lazy=False):
+        # lazy: ABI 6 F_LAZY_STATS (the bench's steps): per-micrograph outputs fetched from HBM
+        # when the Result first reads them
         b, t = (b1, b2, b3)[i], dev_in[i]
         c.submit(b.n_mg, 3, 180, b.box_off, b.id_base, t[0].data_ptr(), t[1].data_ptr(),
-                 t[2].data_ptr(), fl | _lib.F_DEVICE_INPUTS | _lib.F_TIMING,
+                 t[2].data_ptr(), fl | _lib.F_DEVICE_INPUTS | _lib.F_TIMING |
+                 (_lib.F_LAZY_STATS if lazy else 0),
                  dev_meta=(t[3].data_ptr(), t[4].data_ptr()))
 
     # one run in flight per context: wait() with nothing pending raises, and while a submit is
@@ -431,11 +434,11 @@ def _submit_wait_check():
             assert "awaits rgc_wait" in str(e)
     ctxs[0].wait()
 
-    order = [0, 1, 2, 0, 2, 1]
+    order = [0, 1, 2, 0, 2, 1, 0, 1, 0]
     submit(ctxs[0], order[0])
     for j, i in enumerate(order):
         if j + 1 < len(order):
-            submit(ctxs[(j + 1) % 2], order[j + 1])
+            submit(ctxs[(j + 1) % 2], order[j + 1], lazy=j + 1 >= 6)
         got = snap(ctxs[j % 2].wait(), True)
         for f in per_mg:
             np.testing.assert_array_equal(got[f], refs[i][f], err_msg=f"{f} batch {i}")

@@ -10,3 +10,10 @@ def test_stencil_covers_every_edge():
     import stencil_check
     missed, total = stencil_check.run(seed=7, n_mg=45)
     assert total > 100000 and missed == 0
+
+
+def test_large_route_stencil_covers_every_edge():
+    """Same property for the large-micrograph route's per-picker grids (k1_bin / k2_pairs)."""
+    import stencil_check
+    missed, total = stencil_check.run(seed=11, n_mg=45, large=True)
+    assert total > 100000 and missed == 0

@@ -6,7 +6,10 @@ Columns >= 1.08 B wide, rows >= 0.54 B tall; a box searches its column and the n
 column on the side of its half of the column (f32 product, as the kernel), rows cy-1..cy+1.
 Random micrographs with integer, fractional and near-threshold clustered coordinates.
 
-  python tools/stencil_check.py [seed] [micrographs]
+The large-micrograph route's k1_bin / k2_pairs plan (f64 keys, row height h, column width 2 h
+within bin_budget) is restated by plan_large / missed_large.
+
+  python tools/stencil_check.py [seed] [micrographs] [large]
 """
 import sys
 
@@ -64,7 +67,48 @@ def missed(xs, ys, B):
     return miss, tot
 
 
-def run(seed=0, n_mg=300):
+def plan_large(xs, ys, B, n, K=1):
+    """k1_bin's plan (rgc_kernels.hip, the large-micrograph route): f64, row height h, column
+    width 2 h, K gx gy <= bin_budget(n)."""
+    budget = min(2 * n + 64, 65528)
+    per = budget // K
+    mnx, mny = xs.min(), ys.min()
+    ex, ey = xs.max() - mnx, ys.max() - mny
+    h = max(0.54 * B * (1.0 + 1e-9), np.sqrt(0.5 * ex * ey / per), max(0.5 * ex, ey) / per)
+    while True:
+        fx, fy = np.floor(ex / (2.0 * h)) + 1.0, np.floor(ey / h) + 1.0
+        if fx * fy <= per:
+            break
+        h *= 1.0625
+    icl, icly = 1.0 / (2.0 * h), 1.0 / h
+    if icl * (1.08 * B) > 1.0:
+        icl = 1.0 / (1.08 * B)
+    if icly * (0.54 * B) > 1.0:
+        icly = 1.0 / (0.54 * B)
+    return mnx, mny, icl, icly, int(fx), int(fy)
+
+
+def missed_large(xs, ys, B):
+    """(missed pairs, JI > 0.3 pairs) of k2_pairs' stencil (f64 keys and half test)."""
+    mnx, mny, icl, icly, gx, gy = plan_large(xs, ys, B, len(xs))
+    u = (xs - mnx) * icl
+    cx = np.minimum(np.floor(u), gx - 1).astype(int)
+    cy = np.minimum(np.floor((ys - mny) * icly), gy - 1).astype(int)
+    c0 = cx - ((u - cx) < 0.5).astype(int)
+    miss = tot = 0
+    for i in range(len(xs)):
+        ox = np.maximum((np.minimum(xs[i], xs) + B) - np.maximum(xs[i], xs), 0)
+        oy = np.maximum((np.minimum(ys[i], ys) + B) - np.maximum(ys[i], ys), 0)
+        inter = ox * oy
+        e = np.flatnonzero(inter / ((2 * B * B) - inter) > 0.3)
+        e = e[e != i]
+        tot += len(e)
+        ok = ((cx[e] == c0[i]) | (cx[e] == c0[i] + 1)) & (np.abs(cy[e] - cy[i]) <= 1)
+        miss += int((~ok).sum())
+    return miss, tot
+
+
+def run(seed=0, n_mg=300, large=False):
     rng = np.random.default_rng(seed)
     M = T = 0
     for it in range(n_mg):
@@ -80,7 +124,7 @@ def run(seed=0, n_mg=300):
             d = (7 / 13) * B * (1 - rng.uniform(0, 1e-3, (n // 4, 2))) * rng.choice([-1, 1], (n // 4, 2))
             pts = np.concatenate([base, base + d, base + d * [1, 0], base + d * [0, 1]])
             xs, ys = pts[:, 0], pts[:, 1]
-        m, t = missed(xs, ys, B)
+        m, t = (missed_large if large else missed)(xs, ys, B)
         M += m
         T += t
     return M, T
@@ -89,6 +133,6 @@ def run(seed=0, n_mg=300):
 if __name__ == "__main__":
     seed = int(sys.argv[1]) if len(sys.argv) > 1 else 0
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 300
-    m, t = run(seed, n)
+    m, t = run(seed, n, len(sys.argv) > 3 and sys.argv[3] == "large")
     print(f"missed {m} of {t} JI > 0.3 pairs")
     sys.exit(1 if m else 0)
