@@ -21,6 +21,13 @@ constexpr int NW = WG / 64;
 // pointers, so their accesses stay global_load / global_store.
 template <typename T>
 using gptr = __attribute__((address_space(1))) T*;
+#ifdef RGC_X_NODETACH   // timing experiment: plain kernel-argument values
+template <typename T>
+__device__ __forceinline__ gptr<T> gdetach(T* p) { return (gptr<T>)p; }
+__device__ __forceinline__ double sdetach(double v) { return v; }
+__device__ __forceinline__ int sdetach(int v) { return v; }
+__device__ __forceinline__ int64_t sdetach(int64_t v) { return v; }
+#else
 template <typename T>
 __device__ __forceinline__ gptr<T> gdetach(T* p) {
   uint64_t v = (uint64_t)p, r;
@@ -42,6 +49,7 @@ __device__ __forceinline__ int64_t sdetach(int64_t v) {
   asm volatile("s_mov_b64 %0, %1" : "=s"(r) : "s"(v));
   return r;
 }
+#endif
 
 
 // ----------------------------------------------------------------------------- block reductions

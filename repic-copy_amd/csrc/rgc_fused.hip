@@ -868,6 +868,15 @@ __device__ __forceinline__ bool p4_tri(const FShared& S, FusedHdr& H, char* q, i
   return H.trifail == 0;
 }
 
+// P2: boxes with up to FILL_FAST forward edges have their targets kept by the count (the
+// last two in cnt, the first of three in the CC-size slot, zero until P3); the fill writes
+// them without walking the stencil again
+#ifdef RGC_X_T3
+constexpr int FILL_FAST = 3;
+#else
+constexpr int FILL_FAST = 2;
+#endif
+
 // Candidates of a box: the 2x3 cell stencil at its cell in the grid of every HIGHER picker
 // (forward edges only): columns cx, cx + 1 from cx = its column - 1 or its column (by the
 // half of the column the box lies in), rows y0..y1, i.e. up to 2 (K - 1 - p) ranges of
@@ -951,8 +960,8 @@ __device__ __forceinline__ bool edge_test(double2 a, double2 b, double B, double
 template <int K, bool W>
 __device__ __forceinline__ int pairs_count(const Stencil& st, const FShared& S, const GridU& H,
                                            double B, double two_b2, double i_lo, double i_hi,
-                                           uint32_t* mask_out) {
-  uint32_t mask = 0, pk = 0;
+                                           uint32_t* mask_out, uint32_t* first_out) {
+  uint32_t mask = 0, pk = 0, first = 0;
   int cnt = 0, kk = 0;
   // f32 layout: reject in f32 first.  An edge needs both overlaps > (6/13) B, i.e. |dx| and
   // |dy| < (7/13) B = 0.5385 B; the f32 difference of two exact f32 values is within 2^-24 of
@@ -976,6 +985,7 @@ __device__ __forceinline__ int pairs_count(const Stencil& st, const FShared& S, 
                           i_hi);
         }
         if (e) {
+          first = cnt == 0 ? (uint32_t)t : first;
           ++cnt;
           mask |= (kk < 32) ? (1u << kk) : 0u;
           pk = (pk << 16) | (uint32_t)t;
@@ -983,7 +993,8 @@ __device__ __forceinline__ int pairs_count(const Stencil& st, const FShared& S, 
       }
     }
   }
-  *mask_out = cnt <= 2 ? pk : mask;
+  *mask_out = cnt <= FILL_FAST ? pk : mask;
+  *first_out = first;
   return cnt;
 }
 
@@ -991,8 +1002,8 @@ __device__ __forceinline__ int pairs_count(const Stencil& st, const FShared& S, 
 template <int K>
 __device__ __forceinline__ int pairs_count_int(const Stencil& st, const FShared& S,
                                                const GridU& H, float Bf, float Tf,
-                                               uint32_t* mask_out, int ts = 0) {
-  uint32_t mask = 0, pk = 0;
+                                               uint32_t* mask_out, uint32_t* first_out) {
+  uint32_t mask = 0, pk = 0, first = 0;
   int cnt = 0, kk = 0;
   const float ax = (float)st.a.x, ay = (float)st.a.y;
 #ifdef RGC_X_P2A
@@ -1017,6 +1028,7 @@ __device__ __forceinline__ int pairs_count_int(const Stencil& st, const FShared&
       const float xo = fmaxf(Bf - fabsf(ax - bf.x), 0.0f);
       const float yo = fmaxf(Bf - fabsf(ay - bf.y), 0.0f);
       if (xo * yo > Tf) {
+        first = cnt == 0 ? (uint32_t)t : first;
         ++cnt;
         mask |= (kk < 32) ? (1u << kk) : 0u;
         pk = (pk << 16) | (uint32_t)t;
@@ -1034,22 +1046,17 @@ __device__ __forceinline__ int pairs_count_int(const Stencil& st, const FShared&
         const float xo = fmaxf(Bf - fabsf(ax - bf.x), 0.0f);
         const float yo = fmaxf(Bf - fabsf(ay - bf.y), 0.0f);
         if (xo * yo > Tf) {
+          first = cnt == 0 ? (uint32_t)t : first;
           ++cnt;
           mask |= (kk < 32) ? (1u << kk) : 0u;
           pk = (pk << 16) | (uint32_t)t;
-#ifdef RGC_X_CNTUNION   // experiment: the CC unions in the count pass
-          S.flags[t] = 1;
-          uf_union_lds(S.parent, (uint32_t)ts, (uint32_t)t);
-#endif
         }
       }
     }
   }
-#ifdef RGC_X_CNTUNION
-  if (cnt) S.flags[ts] = 1;
 #endif
-#endif
-  *mask_out = cnt <= 2 ? pk : mask;
+  *mask_out = cnt <= FILL_FAST ? pk : mask;
+  *first_out = first;
   return cnt;
 }
 
@@ -1101,10 +1108,13 @@ __device__ __forceinline__ void put_stats(const FusedArgs& A, int m, int status,
   A.o.n_edges[m] = edges;
   A.o.clique_base[m] = base;
   A.o.clique_cnt[m] = C;
-  if (status == 0 || status == RGC_ST_NO_CLIQUES || status == RGC_ST_NO_EDGES)
+  if (status == 0 || status == RGC_ST_NO_CLIQUES || status == RGC_ST_NO_EDGES) {
+#if !defined(RGC_X_NORESV) && !defined(RGC_X_NOEDGESUM)
     atomicAdd(A.cursor + 1, (unsigned long long)edges);
-  else   // needs another pass: counted, so a run's totals alone tell the host (lazy stats)
+#endif
+  } else {   // needs another pass: counted, so a run's totals alone tell the host (lazy stats)
     atomicAdd(A.cursor + 4, 1ull);
+  }
 }
 
 // Waves per SIMD the register allocator targets.  K = 3 fits 64 VGPRs (4 small spills) for 8
@@ -1424,12 +1434,13 @@ void k_fused(FusedArgs A) {
     if (ts >= n) continue;
     Stencil st;
     stencil_setup<K, W>(st, ts, S, G);
-    uint32_t mask;
+    uint32_t mask, first;
     int ec;
-    if constexpr (!W) ec = pairs_count_int<K>(st, S, G, (float)B, (float)ti, &mask, ts);
-    else ec = pairs_count<K, W>(st, S, G, B, two_b2, i_lo, i_hi, &mask);
+    if constexpr (!W) ec = pairs_count_int<K>(st, S, G, (float)B, (float)ti, &mask, &first);
+    else ec = pairs_count<K, W>(st, S, G, B, two_b2, i_lo, i_hi, &mask, &first);
     S.fwd[ts] = (uint16_t)ec;
     S.cnt[ts] = mask;
+    if (FILL_FAST == 3 && ec == 3) S.vrank[ts] = (uint16_t)first;
   }
   __syncthreads();
   STAMP(3);   // count
@@ -1453,43 +1464,94 @@ void k_fused(FusedArgs A) {
 #else
     const bool src_ok = 2 * E <= A.ecap;
 #endif
-#ifdef RGC_X_CNTUNION   // (integer layout: unions already done by the count)
-    constexpr bool cnt_union = !W;
-#else
-    constexpr bool cnt_union = false;
-#endif
     uint16_t* esrc = S.dst + E;
+    // Boxes with more than two targets walk their stencil again.  Done in place, every wave
+    // holding one such box pays for the walk (one in four boxes with edges on C2: nearly every
+    // wave); the RGC_X_SLOWLIST experiment lists them behind esrc (room permitting) and walks
+    // them densely, a thread per listed box, after a barrier (H.V, unused until P5, counts the
+    // list): 3 % fewer VALU instructions on C2, no faster, C4 slower.
+    uint16_t* slow = S.dst + 2 * E;
+#ifdef RGC_X_SLOWLIST   // (fewer VALU instructions, not faster: profiles/r04h_ab_*, r04i_*)
+    const int lcap = src_ok ? A.ecap - 2 * E : 0;
+#else
+    const int lcap = 0;
+#endif
+    auto fill_walk = [&](int i, int base, int cnt) {
+      Stencil st;
+      stencil_setup<K, W>(st, i, S, G);
+      pairs_fill<K, W>(st, S, G, S.cnt[i], S.dst + base, cnt, B, two_b2, i_lo, i_hi);
+    };
     for (int r0 = 0, odd = 0; r0 < n; r0 += FWG, odd ^= 1) {   // same order as the count
       const int ts = odd ? r0 + FWG - 1 - tid : r0 + tid;
-      if (ts >= n) continue;
-      const int i = ts;
-      const int base = S.fwd[i], cnt = (int)S.fwd[i + 1] - base;
-      if (cnt == 0) continue;
-      uint16_t* d = S.dst + base;
-      const uint32_t cw0 = S.cnt[ts];
-      if (cnt <= 2) {   // the count kept the targets themselves (ascending)
-        d[0] = (uint16_t)(cnt == 2 ? cw0 >> 16 : cw0);
-        if (cnt == 2) d[1] = (uint16_t)cw0;
-      } else {
-        Stencil st;
-        stencil_setup<K, W>(st, ts, S, G);
-        pairs_fill<K, W>(st, S, G, cw0, d, cnt, B, two_b2, i_lo, i_hi);
-      }
-      S.flags[i] = 1;
-      if (cnt_union) {
-      } else if (src_ok) {
-        for (int e = 0; e < cnt; ++e) esrc[base + e] = (uint16_t)i;
-      } else {
-        for (int e = 0; e < cnt; ++e) {
-          S.flags[d[e]] = 1;
-          uf_union_lds(S.parent, (uint32_t)i, (uint32_t)d[e]);
+      bool listed = false;
+      if (ts < n) {
+        const int i = ts;
+        const int base = S.fwd[i], cnt = (int)S.fwd[i + 1] - base;
+        if (cnt > 0) {
+          uint16_t* d = S.dst + base;
+          if (cnt <= 2) {   // the count kept the targets themselves (ascending)
+            const uint32_t cw0 = S.cnt[ts];
+            d[0] = (uint16_t)(cnt == 2 ? cw0 >> 16 : cw0);
+            if (cnt == 2) d[1] = (uint16_t)cw0;
+          } else if (FILL_FAST == 3 && cnt == 3) {
+            const uint32_t cw0 = S.cnt[ts];
+            d[0] = S.vrank[ts];
+            S.vrank[ts] = 0;   // (CC-size slot: zero for P3)
+            d[1] = (uint16_t)(cw0 >> 16);
+            d[2] = (uint16_t)cw0;
+          } else if (lcap > 0) {
+            listed = true;
+          } else {
+            fill_walk(i, base, cnt);
+          }
+          S.flags[i] = 1;
+          if (listed) {
+          } else if (src_ok) {
+            for (int e = 0; e < cnt; ++e) esrc[base + e] = (uint16_t)i;
+          } else {
+            for (int e = 0; e < cnt; ++e) {
+              S.flags[d[e]] = 1;
+              uf_union_lds(S.parent, (uint32_t)i, (uint32_t)d[e]);
+            }
+          }
         }
+      }
+      if (lcap > 0) {   // (uniform) one LDS atomic per wave for its listed boxes
+        const unsigned long long bal = __ballot(listed);
+        if (bal) {
+          const int lane = tid & 63;
+          const int first = __builtin_ctzll(bal);
+          int sb = 0;
+          if (lane == first) sb = (int)atomicAdd(reinterpret_cast<uint32_t*>(&H.V), (uint32_t)__popcll(bal));
+          sb = __builtin_amdgcn_readlane(sb, first);
+          const int slot = sb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+          if (listed) {
+            if (slot < lcap) {
+              slow[slot] = (uint16_t)ts;
+            } else {   // list full (rare): in place
+              const int base = S.fwd[ts], cnt = (int)S.fwd[ts + 1] - base;
+              fill_walk(ts, base, cnt);
+              for (int e = 0; e < cnt; ++e) esrc[base + e] = (uint16_t)ts;
+            }
+          }
+        }
+      }
+    }
+    if (lcap > 0) {
+      __syncthreads();
+      const int ns = min(ufl((int)H.V), lcap);
+      for (int j = tid; j < ns; j += FWG) {
+        const int i = slow[j];
+        const int base = S.fwd[i], cnt = (int)S.fwd[i + 1] - base;
+        fill_walk(i, base, cnt);
+        for (int e = 0; e < cnt; ++e) esrc[base + e] = (uint16_t)i;
       }
     }
     __syncthreads();
     STAMP(5);   // fill
     STOP_AFTER(23);
-    if (src_ok && !cnt_union) {
+    if (src_ok) {
       for (int e = tid; e < E; e += FWG) {
         const uint32_t h = S.dst[e];
         S.flags[h] = 1;
@@ -1498,6 +1560,7 @@ void k_fused(FusedArgs A) {
 #endif
       }
       __syncthreads();
+      if (tid == 0) H.V = 0;   // (the slow-list count; P5 sets V)
     }
     if (A.eu) {
       // RGC_F_EDGES test hook: the edge list with the reference's f64 JI (get_cliques.py:40-46)
@@ -1642,7 +1705,7 @@ void k_fused(FusedArgs A) {
   // queue overflowed
   bool tri = false;
   if constexpr (K == 3) {
-#ifndef RGC_X_NOTRI
+#ifdef RGC_X_TRI   // (slower than the BFS on C2 and C4: profiles/r04f_ab_*)
     tri = p4_tri<NT>(S, H, q, qbytes, n0, get_cc, (uint32_t)target, tid);
 #endif
     if (tri) {
@@ -1714,18 +1777,32 @@ void k_fused(FusedArgs A) {
     A.stamps[(int64_t)blockIdx.x * 16 + 15] = (unsigned long long)C;
   }
 #endif
+  // the output reservation: one returning atomic on the batch cursor per micrograph.  Its
+  // result is first needed by P6, so thread 0 only reads it at the end of P5: the round trip
+  // (microseconds with every CU's workgroups on the one cursor word) overlaps P5
+  unsigned long long resv = 0;
   if (tid == 0) {
     H.C = C;
     if (C == 0) {
       H.status = RGC_ST_NO_CLIQUES;
+    } else if (C > 0x7fffffff) {
+      H.status = RGC_ST_DEFER;   // P6 indexes a micrograph's cliques in 32 bits
     } else {
-      if (C > 0x7fffffff) {
-        H.status = RGC_ST_DEFER;   // P6 indexes a micrograph's cliques in 32 bits
-      } else {
-        const unsigned long long base = atomicAdd(A.cursor, (unsigned long long)C);
-        H.base = (int64_t)base;
-        if ((int64_t)base + C > A.cap) H.status = RGC_ST_OVERFLOW;
-      }
+#ifdef RGC_X_NORESV   // timing experiment: no contended reservation (outputs overlap)
+      resv = (unsigned long long)min((int64_t)blockIdx.x * (A.cap / (int64_t)gridDim.x), A.cap - C);
+#elif defined(RGC_X_RSHARD)   // timing experiment: 8 cursor words 256 B apart (outputs overlap)
+      int vz;
+      asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+      // (counters in the unused tail of the rows array)
+      unsigned long long* ctr = reinterpret_cast<unsigned long long*>(A.rows + (A.cap * K - 8192));
+      resv = atomicAdd(ctr + 64 * (blockIdx.x & 7) + vz, (unsigned long long)C) % (A.cap / 2);
+#else
+      // (a lane-varying zero offset keeps the atomic optimizer's wave-reduction expansion,
+      // which consumes the result at once, off this single-lane atomic)
+      int vz;
+      asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+      resv = atomicAdd(A.cursor + vz, (unsigned long long)C);
+#endif
     }
   }
   __syncthreads();
@@ -1782,10 +1859,15 @@ void k_fused(FusedArgs A) {
       }
       S.vrank[t] = (uint16_t)rk;
     }
+    if (tid == 0) H.base = (int64_t)resv;   // (the reservation's round trip ends here)
     __syncthreads();
+    // every thread reads the base; an output overflow skips P6 (the host regrows and re-runs)
+    const bool overflow = H.base + H.C > A.cap;
+    if (overflow && tid == 0) H.status = RGC_ST_OVERFLOW;
 
     STOP_AFTER(5);
     STAMP(10);  // rank
+    if (!overflow) {
     // ---- P6: stage the clique vertices' scores in LDS, then the ILP epilogue + COO rows with
     // one thread per clique (coalesced output stores).  Cliques come from the P4 queue, whose
     // output index is (root's scanned offset + ordinal within the root): the same order as a
@@ -1907,6 +1989,7 @@ void k_fused(FusedArgs A) {
       }
       __syncthreads();
     }
+    }   // !overflow
   }
   STAMP(12);
   if constexpr (QG) {

@@ -446,16 +446,23 @@ __global__ __launch_bounds__(64) void k_ilp_wave(IlpArgs A, int n_big) {
     // lane-sliced sets: P (candidates), chosen
     uint64_t P = 0, chosen = 0, best_set = 0;
     if (lane < W) P = (lane == W - 1 && (n & 63)) ? ((1ull << (n & 63)) - 1) : ~0ull;
+    // the root's bound: the search stops once the incumbent is within Gurobi's MIPGap (1e-4,
+    // relative; run_ilp.py:50-63 solves with default parameters) of it - status GAP_OK
+    const double root_bound = lag ? fmin(bound(P), lag_bound(P)) : bound(P);
     double best = -1.0, cur = 0.0;
     int depth = 0;
     int64_t nodes = 0;
-    bool exact = true;
+    uint8_t status = RGC_ILP_OPTIMAL;
     for (;;) {
       bool back = false;
-      if (++nodes > A.node_limit) { exact = false; break; }
+      if (++nodes > A.node_limit) { status = RGC_ILP_NODE_LIMIT; break; }
       const uint64_t nz = __ballot(P != 0);
       if (nz == 0) {
-        if (cur > best) { best = cur; best_set = chosen; }
+        if (cur > best) {
+          best = cur;
+          best_set = chosen;
+          if (root_bound - best <= 1e-4 * best && depth > 0) { status = RGC_ILP_GAP_OK; break; }
+        }
         back = true;
       } else if ((lag && cur + lag_bound(P) <= best) || cur + bound(P) <= best) {
         back = true;
@@ -511,9 +518,12 @@ __global__ __launch_bounds__(64) void k_ilp_wave(IlpArgs A, int n_big) {
         const int i = lane * 64 + b;
         if (i >= n) break;
         A.x[m[i]] = (best_set >> b) & 1 ? 1 : 0;
-        A.exact[m[i]] = exact ? 1 : 0;
+        A.exact[m[i]] = status;
       }
     }
+    // GAP_OK: the certified gap at the component's first member (the certification below
+    // leaves such components alone: only NODE_LIMIT ones are flagged)
+    if (status == RGC_ILP_GAP_OK && A.gap && lane == 0) A.gap[m[0]] = fmax(root_bound - best, 0.0);
     wave_sync();
   }
 }

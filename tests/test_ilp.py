@@ -112,17 +112,22 @@ def test_highs_fixture_matches_live_solves():
         assert make_ilp_golden.model_key(A, w) in tab
 
 
-def _check(problems, xs, exact, inexact_gap=None):
-    """Exact components must reach the optimum; with ``inexact_gap`` a micrograph whose solve
-    hit the node limit must be a packing within that relative gap of it."""
+def _check(problems, xs, status, inexact_gap=None):
+    """OPTIMAL micrographs must reach the optimum, GAP_OK ones (a component's search stopped
+    within Gurobi's MIPGap of its bound) be within 1e-4 of it; with ``inexact_gap`` a
+    micrograph whose solve hit the node limit must be a packing within that relative gap."""
     from oracle import ilp_ref
+    from repic_amd.ilp import GAP_OK, OPTIMAL
     uniq, gaps = 0, []
-    for (A, w), x, ex in zip(problems, xs, exact):
+    for (A, w), x, st in zip(problems, xs, status):
         assert ilp_ref.is_packing(A, x)
         w64 = np.asarray(w, np.float64)
         obj = float(np.sum(w64[x == 1]))
         xr, objr = highs(A, w)
-        if not ex:
+        if st == GAP_OK:
+            assert -1e-12 <= (objr - obj) / objr <= 1e-4, (obj, objr)
+            continue
+        if st != OPTIMAL:
             assert inexact_gap is not None
             gaps.append((objr - obj) / objr)
             assert -1e-12 <= gaps[-1] <= inexact_gap, (obj, objr)
@@ -140,9 +145,9 @@ def test_gpu_ilp_matches_exact_solvers_on_golden():
     from repic_amd.ilp import solve_batch
     probs = golden_problems() + golden_problems("syn_k4") + golden_problems("syn_k5")
     ctx = _lib.Context(0)
-    xs, exact = solve_batch(ctx, [a for a, _ in probs], [w for _, w in probs])
+    xs, st = solve_batch(ctx, [a for a, _ in probs], [w for _, w in probs], statuses=True)
     ctx.close()
-    assert _check(probs, xs, exact) >= len(probs) - 2
+    assert _check(probs, xs, st) >= len(probs) - 2
 
 
 @pytest.mark.gpu
@@ -155,10 +160,10 @@ def test_gpu_ilp_matches_exact_solvers_synthetic(cfg_name, n, gap):
     from repic_amd.ilp import solve_batch
     probs = synthetic_problems(cfg_name, n)
     ctx = _lib.Context(0)
-    xs, exact = solve_batch(ctx, [a for a, _ in probs], [w for _, w in probs],
-                            node_limit=1 << 18 if gap else 0)
+    xs, st = solve_batch(ctx, [a for a, _ in probs], [w for _, w in probs],
+                         node_limit=1 << 18 if gap else 0, statuses=True)
     ctx.close()
-    _check(probs, xs, exact, gap)
+    _check(probs, xs, st, gap)
 
 
 @pytest.mark.gpu
@@ -347,14 +352,16 @@ def test_gpu_ilp_full_c5_micrograph():
         r = ctx.run(batch.n_mg, cfg.k, cfg.box, batch.box_off, batch.id_base, batch.x, batch.y,
                     batch.score, _lib.F_HOST_OUTPUTS)
         C, V = int(r.clique_cnt[0]), int(r.n_vert[0])
-        rows = np.asarray(r.rows[:C]).reshape(-1)
+        # (copies: the result arrays are views of the context's buffers, freed by close())
+        rows = np.asarray(r.rows[:C]).reshape(-1).copy()
         w = np.asarray(r.w[:C]).copy()
         A = coo_matrix((np.ones(len(rows), np.int64), (rows, np.repeat(np.arange(C), cfg.k))),
                        shape=(V, C))
         assert C > 500000, C
         t0 = time.time()
-        xs, st, rgap = solve_batch(ctx, [A], [w], statuses=True, gaps=True)
+        xs, st, rgap = solve_batch(ctx, [A], [w], statuses=True, gaps=True, timing=True)
         dt = time.time() - t0
+        print("ILP sections (ms):", [(nm, round(ms, 2)) for nm, ms in ctx.kernel_times()])
     finally:
         ctx.close()
     x = xs[0]

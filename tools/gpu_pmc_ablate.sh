@@ -3,7 +3,8 @@
 # product build run under one SQ counter pass; marginal counts per phase = differences.
 #   make -C repic-copy_amd/csrc ablate && gpurun --timeout 900 -- bash tools/gpu_pmc_ablate.sh TAG [C2] [n_mg] [COUNTERS]
 # COUNTERS (one pass, <= 8 SQ counters): default the issue/stall set; "lane" = VALU lane
-# efficiency per phase (SQ_ACTIVE_INST_VALU, SQ_THREAD_CYCLES_VALU, SQ_INSTS_VALU)
+# efficiency per phase (SQ_ACTIVE_INST_VALU, SQ_THREAD_CYCLES_VALU, SQ_INSTS_VALU).
+# LIBS (glob, default abl/librepic_gc_stop*.so): the libraries measured before the product
 set -e -o pipefail
 TAG=${1:-pmcabl}; CFG=${2:-C2}; NMG=${3:-10000}
 OUT=gpurun_out/$TAG
@@ -11,7 +12,8 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 CNT=${4:-"SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH"}
 [ "$CNT" = lane ] && CNT="SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES"
-for L in abl/librepic_gc_stop*.so repic-copy_amd/repic_amd/librepic_gc.so; do
+LIBS=${LIBS:-"abl/librepic_gc_stop*.so"}
+for L in $LIBS repic-copy_amd/repic_amd/librepic_gc.so; do
   b=$(basename "$L" .so)
   timeout -s KILL 120 rocprofv3 --pmc $CNT --output-format csv -d "$OUT/$b" -o run -- \
     python3 tools/ablate.py "$CFG" "$NMG" 1 "$L" > "$OUT/$b.txt" 2> "$OUT/$b.err" || { tail -20 "$OUT/$b.err"; exit 1; }
