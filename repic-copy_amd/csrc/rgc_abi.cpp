@@ -97,7 +97,9 @@ constexpr int LDS_BLOCKS = 128;
 constexpr int64_t FUSED_MAX_BOXES = 4608;
 // device cursors after the per-micrograph block: [0] clique reservation, [1] edges of finished
 // micrographs, [2] edge-dump reservation (RGC_F_EDGES), [3] spare
-constexpr size_t CUR_BYTES = 64;   // [0] cliques [1] edges [2] edge dump [3] ties [4] deferrals
+// [0] cliques [1] edges [2] edge dump [4] deferrals; [CUR_TIES] ties, on its own 64-B line
+// (its per-wave atomics would queue behind the reservations on cursor[0]'s line)
+constexpr size_t CUR_BYTES = 128;
 // D_MGOUT / H_MGOUT = per-micrograph SoA block, then two cursor slots of CUR_BYTES: a run
 // uses slot cur_slot and its kernel zeroes the other one for the next run (no memset packet)
 static int lds_blocks(int bytes) { return (bytes + LDS_BLOCK - 1) / LDS_BLOCK; }
@@ -758,6 +760,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
       A.ecap_out = c->cap_edges;
       A.tie_list = D<int32_t>(c, D_TIES);
       A.tie_cap = c->cap_cliques;
+      A.esum_n = 0;   // (the host sums the finished micrographs' edges from the stats copy)
       int64_t ties_done = 0;   // entries of earlier passes already resolved
 #ifdef RGC_STAMPS
       TRY(ensure_dev(c, D_STAMPS, 3 * (size_t)n_mg * 16 * 8));
@@ -834,7 +837,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
         HIPCHK(hipGetLastError());
         HIPCHK(hipStreamSynchronize(s));
         const int32_t* fst = ho.status;
-        ties_done = std::min<int64_t>((int64_t)h_cur[3], A.tie_cap);
+        ties_done = std::min<int64_t>((int64_t)h_cur[rgc::CUR_TIES], A.tie_cap);
         ml_off += (int)by.size();
         todo.clear();
         auto check = [&](int32_t m) {
@@ -870,7 +873,16 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
         c->cap_cliques = fused_total + fused_total / 8 + 1024;
       c->n_ev = 0;
     }
-    E_total = (int64_t)h_cur[1];   // finished micrographs
+    // edges of the micrographs the fused passes finished (the stats were copied after each
+    // pass; micrographs never launched hold a previous run's stats, so only launched ones)
+    auto fin_edges = [&](int32_t m) {
+      if (ho.status[m] < RGC_ST_DEFER) E_total += ho.n_edges[m];
+    };
+    if (all0) {
+      for (int32_t m = 0; m < n_mg; ++m) fin_edges(m);
+    } else {
+      for (int32_t m : todo0) fin_edges(m);
+    }
   }
 
   int64_t C_total = fused_total;
@@ -1115,6 +1127,7 @@ static int submit_fast(rgc_ctx* c, const rgc_batch_in* in) {
   A.mg_list = nullptr;
   A.tie_list = D<int32_t>(c, D_TIES);
   A.tie_cap = c->cap_cliques;
+  A.esum_n = n_mg;   // k_fused_ties sums the edges of the finished micrographs (cursor[1])
 #ifdef RGC_STAMPS
   return 0;   // the diagnostic build times through rgc_run only
 #endif

@@ -1108,13 +1108,10 @@ __device__ __forceinline__ void put_stats(const FusedArgs& A, int m, int status,
   A.o.n_edges[m] = edges;
   A.o.clique_base[m] = base;
   A.o.clique_cnt[m] = C;
-  if (status == 0 || status == RGC_ST_NO_CLIQUES || status == RGC_ST_NO_EDGES) {
-#if !defined(RGC_X_NORESV) && !defined(RGC_X_NOEDGESUM)
-    atomicAdd(A.cursor + 1, (unsigned long long)edges);
-#endif
-  } else {   // needs another pass: counted, so a run's totals alone tell the host (lazy stats)
+  // a micrograph that needs another pass is counted, so a run's totals alone tell the host
+  // (lazy stats); the edges of finished ones are summed after the launch (k_fused_ties)
+  if (!(status == 0 || status == RGC_ST_NO_CLIQUES || status == RGC_ST_NO_EDGES))
     atomicAdd(A.cursor + 4, 1ull);
-  }
 }
 
 // Waves per SIMD the register allocator targets.  K = 3 fits 64 VGPRs (4 small spills) for 8
@@ -1176,7 +1173,7 @@ void k_fused(FusedArgs A) {
   S.cbuf = reinterpret_cast<uint16_t*>(smem + L.off_cbuf);
   const int tid = threadIdx.x;
   const int m = A.mg_list ? A.mg_list[blockIdx.x] : (int)blockIdx.x;
-  if (blockIdx.x == 0 && tid < 8 && A.cursor_clear) A.cursor_clear[tid] = 0;   // next run's
+  if (blockIdx.x == 0 && tid < 16 && A.cursor_clear) A.cursor_clear[tid] = 0;   // next run's
 #ifdef RGC_STAMPS
   // diagnostic build only: per-phase s_memtime stamps of thread 0 (never in the product .so)
 #define STAMP(i)                                                                            \
@@ -1212,7 +1209,7 @@ void k_fused(FusedArgs A) {
   c.rows = gdetach(A.rows); c.w = gdetach(A.w); c.conf = gdetach(A.conf);
   c.consensus = gdetach(A.consensus);
   c.members = gdetach(A.members); c.order = gdetach(A.order);
-  c.tie_list = gdetach(A.tie_list); c.tie_count = gdetach(A.cursor) + 3;
+  c.tie_list = gdetach(A.tie_list); c.tie_count = gdetach(A.cursor) + CUR_TIES;
   c.tie_cap = sdetach(A.tie_cap);
   const gptr<const double> ax = gdetach(A.x);
   const gptr<const double> ay = gdetach(A.y);
@@ -1794,7 +1791,9 @@ void k_fused(FusedArgs A) {
       int vz;
       asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
       // (counters in the unused tail of the rows array)
-      unsigned long long* ctr = reinterpret_cast<unsigned long long*>(A.rows + (A.cap * K - 8192));
+      // (64-byte aligned: a misaligned 64-bit atomic faults)
+      unsigned long long* ctr = reinterpret_cast<unsigned long long*>(
+          reinterpret_cast<uintptr_t>(A.rows + (A.cap * K - 8192)) & ~(uintptr_t)63);
       resv = atomicAdd(ctr + 64 * (blockIdx.x & 7) + vz, (unsigned long long)C) % (A.cap / 2);
 #else
       // (a lane-varying zero offset keeps the atomic optimizer's wave-reduction expansion,
@@ -2008,10 +2007,21 @@ void k_fused(FusedArgs A) {
 // Consensus on set-order ties and the --multi_out node order of the cliques the fused kernel
 // appended (fused_epilogue_order): networkx iterates set(sorted(clique)) (get_cliques.py:182-183
 // -> CPython set order of the (x, y, id) node keys, pyset.h), first tied member in that order.
-// Grid-stride over the entries [from, cursor[3]).
+// Grid-stride over the entries [from, cursor[CUR_TIES]).
 template <int K>
 __global__ __launch_bounds__(256) void k_fused_ties(FusedArgs A, int64_t from) {
-  const int64_t n = min((int64_t)__hip_atomic_load(A.cursor + 3, __ATOMIC_RELAXED,
+  if (A.esum_n > 0 && blockIdx.x < 16) {
+    // edges of the finished micrographs into cursor[1]: 16 workgroups, one atomic each
+    __shared__ int64_t red[4];
+    int64_t e = 0;
+    for (int m = blockIdx.x * 256 + threadIdx.x; m < A.esum_n; m += 16 * 256) {
+      const int st = A.o.status[m];
+      if (st == 0 || st == RGC_ST_NO_CLIQUES || st == RGC_ST_NO_EDGES) e += A.o.n_edges[m];
+    }
+    e = block_sum64<256>(e, red);
+    if (threadIdx.x == 0 && e) atomicAdd(A.cursor + 1, (unsigned long long)e);
+  }
+  const int64_t n = min((int64_t)__hip_atomic_load(A.cursor + CUR_TIES, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT), A.tie_cap);
   for (int64_t t = from + (int64_t)blockIdx.x * 256 + threadIdx.x; t < n;
        t += (int64_t)gridDim.x * 256) {

@@ -45,6 +45,9 @@ struct MgStat {
   int n_nodes, cc_cnt, cc_max, status, target, n_vert;
 };
 
+// cursor block word of the set-order tie count (a separate 64-B line from cursor[0])
+constexpr int CUR_TIES = 8;
+
 // internal per-micrograph status codes (0..2 are the public RGC_* codes)
 constexpr int RGC_ST_NO_EDGES = 1;
 constexpr int RGC_ST_NO_CLIQUES = 2;
@@ -97,7 +100,10 @@ struct FusedArgs {
   const double* y;
   const double* score;
   MgOut o;                      // per-micrograph outputs (device)
-  unsigned long long* cursor;   // [0] clique-range reservation, [1] edges of finished mgs
+  // [0] clique-range reservation, [1] edges of finished mgs (summed by k_fused_ties over the
+  // first esum_n micrographs' stats; no per-workgroup atomic: 10k workgroups adding to one
+  // word cost ~8 % of C2's kernel), [2] edge dump, [4] deferrals, [CUR_TIES] ties
+  unsigned long long* cursor;
   // cursors of the context's other run slot: zeroed by block 0 for the next run (no memset
   // packet between runs)
   unsigned long long* cursor_clear;
@@ -122,9 +128,10 @@ struct FusedArgs {
   int qg_nslots, qg_bytes;
   // cliques whose consensus / --multi_out order needs CPython set order (degree ties with
   // 2k < |G|): entries of 4 + k int32 (j lo, j hi, micrograph, top | tie << 16 | multi << 17,
-  // k batch box indices) for k_fused_ties, counted on cursor[3]; tie_cap entries
+  // k batch box indices) for k_fused_ties, counted on cursor[CUR_TIES]; tie_cap entries
   int32_t* tie_list;
   int64_t tie_cap;
+  int esum_n;   // k_fused_ties: micrographs whose finished edges it sums into cursor[1]
 };
 
 int fused_lds_bytes(int nmax, int ecap, bool wide);
@@ -132,7 +139,7 @@ int fused_vgprs(int k, bool wide, int nt);
 bool fused_nt_ok(int k, int nt);
 int launch_fused(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArgs& A, bool wide,
                  int nt);
-// the tie entries [from, cursor[3]) of the fused launches before it (CPython set order)
+// the tie entries [from, cursor[CUR_TIES]) of the fused launches before it (CPython set order)
 int launch_fused_ties(hipStream_t stream, const FusedArgs& A, int64_t from);
 void launch_gather(hipStream_t stream, int n_sub, int k, const int32_t* sub_mg,
                    const int32_t* box_off, const int32_t* sub_box_off, const double* x,

@@ -387,6 +387,8 @@ def _submit_wait_check():
     def snap(r, on_dev):
         d = {f: np.array(getattr(r, f)) for f in per_mg}
         C = int(r.n_cliques)
+        # batch totals (the fast path sums the edges after the launch, k_fused_ties)
+        d["tot"] = (int(r.n_edges), C, int(np.asarray(r.n_edges_mg).sum()))
         for f, dt, w in per_cl:
             v = getattr(r, f)
             v = _d2h(v, C * w, dt) if on_dev else np.asarray(v).reshape(-1)
@@ -442,6 +444,7 @@ def _submit_wait_check():
         got = snap(ctxs[j % 2].wait(), True)
         for f in per_mg:
             np.testing.assert_array_equal(got[f], refs[i][f], err_msg=f"{f} batch {i}")
+        assert got["tot"] == refs[i]["tot"], (got["tot"], refs[i]["tot"])
         for f, _, _ in per_cl:
             for a, e in zip(got[f], refs[i][f]):
                 np.testing.assert_array_equal(a.view(np.uint8), e.view(np.uint8), err_msg=f)
