@@ -182,7 +182,8 @@ typedef struct rgc_ilp_in {
   const int64_t* col_ptr;  /* [n_cols + 1] column c's rows: row_idx[col_ptr[c], col_ptr[c+1]) */
   const int32_t* row_idx;  /* [nnz] global row ids */
   const double* w;         /* [n_cols] objective */
-  int64_t node_limit;      /* branch-and-bound nodes per component (0: 2^22) */
+  int64_t node_limit;      /* branch-and-bound nodes per component (0: 2^22); components of more
+                              than 1024 cliques get node_limit * 1024 / n (work-scaled) */
   uint32_t flags;          /* RGC_F_TIMING */
   double* gap;             /* optional (NULL: not returned), ABI 6: [n_cols] dual bound minus
                             * packing value of column c's component, at the component's first

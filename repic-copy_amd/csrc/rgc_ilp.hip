@@ -453,9 +453,13 @@ __global__ __launch_bounds__(64) void k_ilp_wave(IlpArgs A, int n_big) {
     int depth = 0;
     int64_t nodes = 0;
     uint8_t status = RGC_ILP_OPTIMAL;
+    // node budget in work units: a node costs O(W) (bound passes over P's words), so
+    // components above 1024 cliques get node_limit * 16 / W nodes (a whole C5 micrograph's
+    // medium components ran 27 s at 2^22 nodes each)
+    const int64_t node_cap = A.node_limit * 16 / (W > 16 ? W : 16);
     for (;;) {
       bool back = false;
-      if (++nodes > A.node_limit) { status = RGC_ILP_NODE_LIMIT; break; }
+      if (++nodes > node_cap) { status = RGC_ILP_NODE_LIMIT; break; }
       const uint64_t nz = __ballot(P != 0);
       if (nz == 0) {
         if (cur > best) {
