@@ -200,6 +200,32 @@ __device__ __forceinline__ void uf_union_lds(uint16_t* parent, uint32_t a, uint3
   }
 }
 
+// u32 parents (the dead P2 count words, see P2's union): path halving by plain stores (any
+// ancestor is a valid parent, and parents only ever decrease), linking by atomicMin of the
+// larger root's word to the smaller root - no CAS retry loop, no false conflicts between two
+// u16 halves of one word.  If the larger root was linked meanwhile (old != a), its old parent
+// and b are joined in turn (hooking as in ECL-CC).
+__device__ __forceinline__ uint32_t uf_find32(uint32_t* parent, uint32_t x) {
+  for (;;) {
+    const uint32_t p = lds_ld(parent + x);
+    if (p == x) return x;
+    const uint32_t gp = lds_ld(parent + p);
+    if (gp != p) lds_st(parent + x, gp);
+    x = gp;
+  }
+}
+__device__ __forceinline__ void uf_union32(uint32_t* parent, uint32_t a, uint32_t b) {
+  for (;;) {
+    a = uf_find32(parent, a);
+    b = uf_find32(parent, b);
+    if (a == b) return;
+    if (a < b) { const uint32_t t = a; a = b; b = t; }
+    const uint32_t old = atomicMin(parent + a, b);
+    if (old == a) return;
+    a = old;
+  }
+}
+
 template <int K>
 __device__ __forceinline__ int picker_of(const int (&pb)[K + 1], int i) {
   int p = 0;
@@ -1452,6 +1478,7 @@ void k_fused(FusedArgs A) {
   }
   STAMP(4);   // scan
   STOP_AFTER(22);
+  bool cc32 = false;   // the unions ran on u32 parents in cnt
   if (st2 == 0) {
     // fill each list (already sorted: position order) and record each edge's source in dst's
     // unused tail when it has room; then union the edges one thread per edge (lock-free
@@ -1462,88 +1489,44 @@ void k_fused(FusedArgs A) {
     const bool src_ok = 2 * E <= A.ecap;
 #endif
     uint16_t* esrc = S.dst + E;
-    // Boxes with more than two targets walk their stencil again.  Done in place, every wave
-    // holding one such box pays for the walk (one in four boxes with edges on C2: nearly every
-    // wave); the RGC_X_SLOWLIST experiment lists them behind esrc (room permitting) and walks
-    // them densely, a thread per listed box, after a barrier (H.V, unused until P5, counts the
-    // list): 3 % fewer VALU instructions on C2, no faster, C4 slower.
-    uint16_t* slow = S.dst + 2 * E;
-#ifdef RGC_X_SLOWLIST   // (fewer VALU instructions, not faster: profiles/r04h_ab_*, r04i_*)
-    const int lcap = src_ok ? A.ecap - 2 * E : 0;
-#else
-    const int lcap = 0;
-#endif
     auto fill_walk = [&](int i, int base, int cnt) {
       Stencil st;
       stencil_setup<K, W>(st, i, S, G);
       pairs_fill<K, W>(st, S, G, S.cnt[i], S.dst + base, cnt, B, two_b2, i_lo, i_hi);
     };
+    // with room for esrc the unions run after the fill on u32 parents in cnt (each box's
+    // count word is dead once its own thread has read it): identity parents written here
     for (int r0 = 0, odd = 0; r0 < n; r0 += FWG, odd ^= 1) {   // same order as the count
       const int ts = odd ? r0 + FWG - 1 - tid : r0 + tid;
-      bool listed = false;
-      if (ts < n) {
-        const int i = ts;
-        const int base = S.fwd[i], cnt = (int)S.fwd[i + 1] - base;
-        if (cnt > 0) {
-          uint16_t* d = S.dst + base;
-          if (cnt <= 2) {   // the count kept the targets themselves (ascending)
-            const uint32_t cw0 = S.cnt[ts];
-            d[0] = (uint16_t)(cnt == 2 ? cw0 >> 16 : cw0);
-            if (cnt == 2) d[1] = (uint16_t)cw0;
-          } else if (FILL_FAST == 3 && cnt == 3) {
-            const uint32_t cw0 = S.cnt[ts];
-            d[0] = S.vrank[ts];
-            S.vrank[ts] = 0;   // (CC-size slot: zero for P3)
-            d[1] = (uint16_t)(cw0 >> 16);
-            d[2] = (uint16_t)cw0;
-          } else if (lcap > 0) {
-            listed = true;
-          } else {
-            fill_walk(i, base, cnt);
-          }
-          S.flags[i] = 1;
-          if (listed) {
-          } else if (src_ok) {
-            for (int e = 0; e < cnt; ++e) esrc[base + e] = (uint16_t)i;
-          } else {
-            for (int e = 0; e < cnt; ++e) {
-              S.flags[d[e]] = 1;
-              uf_union_lds(S.parent, (uint32_t)i, (uint32_t)d[e]);
-            }
+      if (ts >= n) continue;
+      const int i = ts;
+      const int base = S.fwd[i], cnt = (int)S.fwd[i + 1] - base;
+      if (cnt > 0) {
+        uint16_t* d = S.dst + base;
+        if (cnt <= 2) {   // the count kept the targets themselves (ascending)
+          const uint32_t cw0 = S.cnt[ts];
+          d[0] = (uint16_t)(cnt == 2 ? cw0 >> 16 : cw0);
+          if (cnt == 2) d[1] = (uint16_t)cw0;
+        } else if (FILL_FAST == 3 && cnt == 3) {
+          const uint32_t cw0 = S.cnt[ts];
+          d[0] = S.vrank[ts];
+          S.vrank[ts] = 0;   // (CC-size slot: zero for P3)
+          d[1] = (uint16_t)(cw0 >> 16);
+          d[2] = (uint16_t)cw0;
+        } else {
+          fill_walk(i, base, cnt);
+        }
+        S.flags[i] = 1;
+        if (src_ok) {
+          for (int e = 0; e < cnt; ++e) esrc[base + e] = (uint16_t)i;
+        } else {
+          for (int e = 0; e < cnt; ++e) {
+            S.flags[d[e]] = 1;
+            uf_union_lds(S.parent, (uint32_t)i, (uint32_t)d[e]);
           }
         }
       }
-      if (lcap > 0) {   // (uniform) one LDS atomic per wave for its listed boxes
-        const unsigned long long bal = __ballot(listed);
-        if (bal) {
-          const int lane = tid & 63;
-          const int first = __builtin_ctzll(bal);
-          int sb = 0;
-          if (lane == first) sb = (int)atomicAdd(reinterpret_cast<uint32_t*>(&H.V), (uint32_t)__popcll(bal));
-          sb = __builtin_amdgcn_readlane(sb, first);
-          const int slot = sb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                     __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-          if (listed) {
-            if (slot < lcap) {
-              slow[slot] = (uint16_t)ts;
-            } else {   // list full (rare): in place
-              const int base = S.fwd[ts], cnt = (int)S.fwd[ts + 1] - base;
-              fill_walk(ts, base, cnt);
-              for (int e = 0; e < cnt; ++e) esrc[base + e] = (uint16_t)ts;
-            }
-          }
-        }
-      }
-    }
-    if (lcap > 0) {
-      __syncthreads();
-      const int ns = min(ufl((int)H.V), lcap);
-      for (int j = tid; j < ns; j += FWG) {
-        const int i = slow[j];
-        const int base = S.fwd[i], cnt = (int)S.fwd[i + 1] - base;
-        fill_walk(i, base, cnt);
-        for (int e = 0; e < cnt; ++e) esrc[base + e] = (uint16_t)i;
-      }
+      if (src_ok) S.cnt[ts] = (uint32_t)ts;
     }
     __syncthreads();
     STAMP(5);   // fill
@@ -1553,12 +1536,12 @@ void k_fused(FusedArgs A) {
         const uint32_t h = S.dst[e];
         S.flags[h] = 1;
 #ifndef RGC_X_NOUNION   // timing experiment only: no unions (CC stats wrong)
-        uf_union_lds(S.parent, esrc[e], h);
+        uf_union32(S.cnt, esrc[e], h);
 #endif
       }
       __syncthreads();
-      if (tid == 0) H.V = 0;   // (the slow-list count; P5 sets V)
     }
+    cc32 = src_ok;
     if (A.eu) {
       // RGC_F_EDGES test hook: the edge list with the reference's f64 JI (get_cliques.py:40-46)
       if (tid == 0) H.base = (int64_t)atomicAdd(A.cursor + 2, (unsigned long long)E);
@@ -1593,7 +1576,7 @@ void k_fused(FusedArgs A) {
     if (!S.flags[i]) continue;
     const int e0 = S.fwd[i], e1 = S.fwd[i + 1];
     S.split[i] = (uint16_t)lb16(S.dst, e0, e1, next_picker_end<K>(c.pp, i));   // every node
-    const uint32_t r = uf_find_lds(S.parent, i);
+    const uint32_t r = cc32 ? uf_find32(S.cnt, i) : uf_find_lds(S.parent, i);
     p16_st(S.parent + i, r);
     atomicAdd(&ccsz[r >> 1], 1u << (16 * (r & 1)));
   }
