@@ -690,7 +690,8 @@ struct BfsLevel {
       CN[e] = cnt;
     }
     __syncthreads();
-    const int64_t nN = ufl64(block_scan_dpp<NT>(CN, (int)nD, H.red64));
+    // (32-bit scan: nD <= 65535 entries of at most n <= 4608 extensions each, < 2^31)
+    const int64_t nN = ufl(block_scan_dpp32<NT>(CN, (int)nD, H.redi));
     constexpr bool last = D + 1 == K;
     const int nb = ufl((lvl[D] + 4 * (int)nD + 3) & ~3);   // next level starts here
     if (K >= 4) {
@@ -773,7 +774,7 @@ __device__ __forceinline__ BfsOut<K> bfs_cliques(const FShared& S, FusedHdr& H, 
     cnt[i] = root_ok(r) ? (uint32_t)(seg_end(r) - S.fwd[r]) : 0u;
   }
   __syncthreads();
-  const int64_t n2 = ufl64(block_scan_dpp<NT>(cnt, nr, H.red64));
+  const int64_t n2 = ufl(block_scan_dpp32<NT>(cnt, nr, H.redi));   // (< n^2 < 2^31)
   constexpr bool last = K == 2;
   if (K >= 4) out.fit = fminf(bfs_fit(n2, 65535), bfs_fit(n2 * (last ? 6 : 4), qbytes));
   if (n2 > 65535 || n2 * (last ? 6 : 4) > qbytes) {
