@@ -677,12 +677,17 @@ struct BfsLevel {
       const int m = mm[D - 1];
       const int lo = S.fwd[m], hi = seg_end<REWALK>(S, pp, m);
       uint32_t mask = 0, cnt = 0;
+      // an extension h (picker D) lies past member mm[d]'s first segment (picker d + 1 < D):
+      // search from split (dead in REWALK: the whole list)
+      int slo[K > 2 ? K - 2 : 1];
+#pragma unroll
+      for (int d = 0; d < D - 1; ++d) slo[d] = REWALK ? (int)S.fwd[mm[d]] : (int)S.split[mm[d]];
       for (int t = lo; t < hi; ++t) {
         const int h = S.dst[t];
         bool ok = true;
 #pragma unroll
         for (int d = 0; d < D - 1; ++d)
-          ok = ok && contains16(S.dst, S.fwd[mm[d]], S.fwd[mm[d] + 1], h);
+          ok = ok && contains16(S.dst, slo[d], S.fwd[mm[d] + 1], h);
         cnt += ok ? 1u : 0u;
         mask |= (ok && t - lo < 32) ? (1u << (t - lo)) : 0u;
       }
