@@ -142,6 +142,48 @@ __global__ __launch_bounds__(WG) void k5n_build(CliqueArgs A) {
 template <int K, bool FIRST, bool LEAF, bool FILL>
 __global__ __launch_bounds__(WG) void k5l(CliqueArgs A, LevelArgs L) {
   const int64_t i = (int64_t)blockIdx.x * WG + threadIdx.x;
+  if constexpr (LEAF && !FILL && !FIRST) {
+    // leaf count + clique-vertex marks.  A wave's prefixes come grouped by root (parent order),
+    // and a root's prefixes share most of their members: the marks (members of every prefix
+    // with a leaf, and its leaves, as lanes of the root's forward list) are OR-ed over each
+    // run of equal roots in the wave (segmented DPP-free shuffle scan), and the run's last
+    // lane stores each marked member once - instead of every prefix storing its K - 2 members
+    // and all its leaves (C5: ~62 M cliques' worth of scattered byte stores per step).
+    const int lane = threadIdx.x & 63;
+    const bool valid = i < L.n_items;
+    int r = -1 - lane;   // (invalid lanes: roots of their own, never joined)
+    uint64_t bits = 0;
+    int64_t lo = 0;
+    if (valid) {
+      r = L.in_root[i];
+      const uint64_t P = L.in_P[i];
+      const uint64_t c = L.in_M[i] & picker_lanes(A.rbound[r], L.D + 1);
+      L.cnt[i] = __popcll(c);
+      lo = A.fwd_off[r];
+      if (c) {
+        bits = c;
+#pragma unroll
+        for (int q = 0; q < K - 2; ++q) bits |= 1ull << ((P >> (6 * q)) & 63);
+      }
+    }
+#pragma unroll
+    for (int sft = 1; sft < 64; sft <<= 1) {
+      const uint64_t ob = __shfl_up(bits, sft, 64);
+      const int orr = __shfl_up(r, sft, 64);
+      if (lane >= sft && orr == r) bits |= ob;
+    }
+    const int nr = __shfl_down(r, 1, 64);
+    const bool tail = lane == 63 || nr != r;
+    if (valid && tail && bits) {
+      A.in_clique[r] = 1;
+      while (bits) {
+        const int v = __builtin_ctzll(bits);
+        bits &= bits - 1;
+        A.in_clique[A.e_dst[lo + v]] = 1;
+      }
+    }
+    return;
+  }
   if (i >= L.n_items) return;
   int r;
   uint64_t M, P;

@@ -205,6 +205,14 @@ __global__ __launch_bounds__(WG) void k2_pairs(int N, int k, double B, double tw
   int cnt = 0;
   int64_t base = 0;
   if (FILL) base = fwd_off[g];
+  // fill: up to FILL_REGS targets stay in registers and are sorted by a compare-exchange
+  // network (an insertion sort through global memory costs a dependent L2 round trip per
+  // shift); longer lists, and the RGC_F_EDGES dump with its JIs, go through e_dst
+  constexpr int FILL_REGS = 8;
+  const bool reg = FILL && e_ji == nullptr;
+  int rk[FILL_REGS];
+#pragma unroll
+  for (int i = 0; i < FILL_REGS; ++i) rk[i] = INT32_MAX;
   const int key = bin_key(G, p, xa, ya);
   if (key < G.nkey && p + 1 < k) {
     const int cell = key - p * G.ncell;
@@ -241,8 +249,22 @@ __global__ __launch_bounds__(WG) void k2_pairs(int N, int k, double B, double tw
           }
           if (e) {
             if (FILL) {
-              e_dst[base + cnt] = sbox[v];
-              if (e_ji) e_ji[base + cnt] = jaccard(xa, ya, xb, yb, B, two_b2);
+              if (reg) {   // the first FILL_REGS targets in a register shift chain
+                if (cnt == FILL_REGS) {   // more: spill them in arrival order, then write through
+#pragma unroll
+                  for (int i = 0; i < FILL_REGS; ++i) e_dst[base + i] = rk[FILL_REGS - 1 - i];
+                }
+                if (cnt < FILL_REGS) {
+#pragma unroll
+                  for (int i = FILL_REGS - 1; i > 0; --i) rk[i] = rk[i - 1];
+                  rk[0] = sbox[v];
+                } else {
+                  e_dst[base + cnt] = sbox[v];
+                }
+              } else {
+                e_dst[base + cnt] = sbox[v];
+                if (e_ji) e_ji[base + cnt] = jaccard(xa, ya, xb, yb, B, two_b2);
+              }
             }
             ++cnt;
           }
@@ -252,6 +274,11 @@ __global__ __launch_bounds__(WG) void k2_pairs(int N, int k, double B, double tw
   }
   if (!FILL) {
     fwd_cnt[g] = cnt;
+  } else if (reg && cnt <= FILL_REGS) {
+    cmpnet_apply<FILL_REGS, false>(rk);   // ascending; unused slots hold INT32_MAX
+#pragma unroll
+    for (int i = 0; i < FILL_REGS; ++i)
+      if (i < cnt) e_dst[base + i] = rk[i];
   } else {
     // insertion sort by target box (each picker's segment arrives in cell order)
     for (int i = 1; i < cnt; ++i) {
