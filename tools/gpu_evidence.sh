@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 for C in $CFGS; do
   echo "== $C stats"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$C" -o run -- \
-    python3 bench.py --config $C --no-cpu-baseline > "$OUT/bench_prof_$C.json" 2> "$OUT/prof_$C.err" \
+    python3 bench.py --config $C --no-cpu-baseline --by-config none > "$OUT/bench_prof_$C.json" 2> "$OUT/prof_$C.err" \
     || { tail -30 "$OUT/prof_$C.err"; exit 1; }
   find "$OUT/prof_$C" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats_$C.csv" \;
   head -8 "$OUT/kernel_stats_$C.csv"
@@ -23,7 +23,7 @@ for C in $CFGS; do
 done
 for C in $CFGS; do
   echo "== $C bench + cpu baseline"
-  timeout -k 10 400 python3 -u bench.py --config $C > "$OUT/bench_$C.json" 2> "$OUT/bench_$C.err" \
+  timeout -k 10 400 python3 -u bench.py --config $C --by-config none > "$OUT/bench_$C.json" 2> "$OUT/bench_$C.err" \
     || { tail -30 "$OUT/bench_$C.err"; exit 1; }
   python3 -c "import json;d=json.load(open('$OUT/bench_$C.json'));r=d['roofline'];print('$C', round(d['value']), round(d['ms_per_step'],4), round(r['frac'],4), d.get('cpu_baseline',{}).get('value'))"
 done
