@@ -82,9 +82,11 @@ def pmc_record(config):
     return None, None
 
 
-def roofline_evidence(rec, kernel, alg_bytes, kernel_ms):
+def roofline_evidence(rec, kernel, alg_bytes, kernel_ms, dv_kernel=None):
     """(traffic bytes per launch/step, measured HBM fraction, limiter text) from the config's
-    committed counters; the limiter names what the counters show, not a fixed claim."""
+    committed counters; the limiter names what the counters show, not a fixed claim.  The
+    multi-kernel route's issue counters are those of dv_kernel, its longest kernel (the same
+    ones derived_bound reads)."""
     if rec is None:
         return None, None, ("unmeasured for this library build: no profiles/*_traffic.json "
                             "with its sha256 for this config")
@@ -94,7 +96,8 @@ def roofline_evidence(rec, kernel, alg_bytes, kernel_ms):
             return None, None, "no k_fused counters in the matching PMC file"
         traffic, dv = k["traffic"], k.get("derived", {})
     else:
-        traffic, dv = rec.get("step_traffic"), {}
+        traffic = rec.get("step_traffic")
+        dv = rec.get("kernels", {}).get(dv_kernel, {}).get("derived", {}) if dv_kernel else {}
         if traffic is None:
             return None, None, "no per-step traffic in the matching PMC file"
     hbm = traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
@@ -108,6 +111,8 @@ def roofline_evidence(rec, kernel, alg_bytes, kernel_ms):
         parts.append(f"{dv['waves_per_cu']:.1f} resident waves/CU")
     if "lane_eff" in dv:
         parts.append(f"VALU lane efficiency {100 * dv['lane_eff']:.0f}%")
+    if dv and kernel != "k_fused":
+        parts.append(f"issue counters of {dv_kernel}, the route's longest kernel")
     bound = ("VALU issue" if dv.get("valu_busy", 0) > 0.6 and hbm < 0.5 else
              "HBM bandwidth" if hbm >= 0.5 else "latency (neither VALU nor HBM saturated)")
     if not dv:
@@ -460,7 +465,8 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     rec, traffic_src = pmc_record(config)
     kind = "k_fused" if dom == "k_fused" else "route"
-    traffic, hbm_frac, limiter = roofline_evidence(rec, kind, dom_bytes, dom_ms)
+    dv_kernel = "k_fused" if kind == "k_fused" else max(avg, key=avg.get)
+    traffic, hbm_frac, limiter = roofline_evidence(rec, kind, dom_bytes, dom_ms, dv_kernel)
     out = {
         "value": value, "unit": "micrographs/s", "n_gpus": world, "steps": steps,
         "warmup": warmup, "ms_per_step": elapsed / steps * 1e3,
@@ -472,8 +478,7 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
                    "steps_in_flight": 2 if pipeline else 1},
         "edges_per_sec": tot_e * steps / elapsed,
         "totals": {"micrographs": tot_mg, "edges": tot_e, "cliques": tot_c},
-        "roofline": {"bound": derived_bound(rec, kind, dom_bytes, dom_ms,
-                                            "k_fused" if kind == "k_fused" else max(avg, key=avg.get)),
+        "roofline": {"bound": derived_bound(rec, kind, dom_bytes, dom_ms, dv_kernel),
                      "priced_against": "hbm (no contraction: no MFMA roofline applies)",
                      "kernel": dom, "achieved": achieved,
                      # the limiter (and bound) come from this build's committed PMC counters
