@@ -209,6 +209,10 @@ def _counter_device(ctx):
 CHUNK_MG = 1024
 # micrographs per writer task
 GROUP_MG = 64
+# ... or fewer when their cliques reach this many: a group is one writer thread's task, so a
+# chunk of large micrographs (C5: ~1 M cliques each) is spread over the writer threads instead
+# of leaving one thread a multi-second tail
+GROUP_CLIQUES = 1 << 18
 
 
 class _Run:
@@ -272,6 +276,7 @@ class _Run:
         share = (ch.parse_s + getattr(ch, "dev_s", 0.0)) / max(1, len(ch.mgs))
         t0 = time.time()
         items, slots = [], []
+        gcl = 0
         raise_at = None
         for i, mg in enumerate(mgs):
             print(f"\n--- {mg.base} ---\n")
@@ -285,10 +290,12 @@ class _Run:
             else:
                 items.append((mg.base, 0, 0, 0, 0, share, None))
                 slots.append(mg.slot)
+                gcl += int(ch.res.clique_cnt[mg.slot])
                 self.stats["micrographs"] += 1
-            if len(items) >= GROUP_MG:
+            if len(items) >= GROUP_MG or gcl >= GROUP_CLIQUES:
                 self._submit_group(ch, items, slots, writer)
                 items, slots = [], []
+                gcl = 0
         if items:
             self._submit_group(ch, items, slots, writer)
         self.stats["write_s"] += time.time() - t0

@@ -21,6 +21,7 @@ from repic_amd.ingest import DirIndex, list_methods, micrograph_names
 class _FakeRes:
     def __init__(self, status):
         self.status = status
+        self.clique_cnt = np.zeros(len(status), np.int64)
 
 
 class _FakeWriter:
