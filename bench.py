@@ -406,6 +406,9 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
 
         submit(ctxs[0], timed(0))
         for i in range(n):
+            # drop step i-1's Result before its context is reused: a Result still referenced
+            # at the next submit makes the context hand its host buffers over to it
+            r = None
             if i + 1 < n:
                 submit(ctxs[(i + 1) % 2], timed(i + 1))
             c = ctxs[i % 2]

@@ -18,7 +18,8 @@
  *
  * Conventions: plain pointers and sizes, no torch types.  Returns 0 on success and a
  * negative code on error (message in rgc_last_error(), thread-local).  Outputs are owned
- * by the context and stay valid until the next rgc_run on it or rgc_ctx_destroy.
+ * by the context and stay valid until the next rgc_run on it or rgc_ctx_destroy, unless the
+ * caller takes over their host buffers with rgc_detach_host (ABI 7).
  */
 #ifndef REPIC_GC_H
 #define REPIC_GC_H
@@ -28,7 +29,7 @@
 extern "C" {
 #endif
 
-#define RGC_ABI_VERSION 6
+#define RGC_ABI_VERSION 7
 
 /* flags for rgc_batch_in.flags */
 #define RGC_F_GET_CC         1u  /* --get_cc   (get_cliques.py:151-156) */
@@ -135,6 +136,15 @@ int rgc_wait(rgc_ctx* ctx, rgc_batch_out* out);
 /* ABI 6: after rgc_wait of an RGC_F_LAZY_STATS run, copy its per-micrograph outputs into the
  * host arrays *out points to (a no-op for any other run).  Valid until the next run on ctx. */
 int rgc_fetch_stats(rgc_ctx* ctx);
+/* ABI 7: ownership hand-off of the last run's host outputs.  rgc_detach_host moves every
+ * pinned host buffer of the context (the per-micrograph arrays, the RGC_F_HOST_OUTPUTS
+ * per-clique arrays, a lazy run's stats, fetched first) into *block: the pointers the last
+ * rgc_batch_out holds stay valid, and stay unchanged, until rgc_host_block_free(*block), even
+ * after further runs or rgc_ctx_destroy; the context allocates new buffers for its next run.
+ * Fails while a submitted run awaits rgc_wait.  (repic_amd/_lib.py calls it only when a
+ * Result of the last run is still referenced when the next run starts or the context closes.) */
+int rgc_detach_host(rgc_ctx* ctx, void** block);
+void rgc_host_block_free(void* block);
 /* Per-kernel device milliseconds of the last rgc_run with RGC_F_TIMING; returns the count. */
 int rgc_kernel_times(rgc_ctx* ctx, int max_n, float* ms, const char** names);
 

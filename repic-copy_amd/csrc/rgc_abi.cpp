@@ -1331,6 +1331,37 @@ int rgc_fetch_stats(rgc_ctx* c) {
   return 0;
 }
 
+// ABI 7: the host buffers the last run's outputs point into, handed to the caller
+struct rgc_host_block {
+  std::vector<void*> bufs;
+};
+
+int rgc_detach_host(rgc_ctx* c, void** block) {
+  if (!c || !block) return fail("null argument");
+  *block = nullptr;
+  if (c->pend) return fail("rgc_detach_host: a submitted run awaits rgc_wait on this context");
+  HIPCHK(hipSetDevice(c->device));
+  TRY(rgc_fetch_stats(c));   // a lazy run's per-micrograph block lands in the detached buffer
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (c->copy_stream) HIPCHK(hipStreamSynchronize(c->copy_stream));
+  rgc_host_block* b = new rgc_host_block();
+  for (auto& h : c->h) {
+    if (h.p) b->bufs.push_back(h.p);
+    h.p = nullptr;   // the next run allocates fresh pinned buffers
+    h.cap = 0;
+  }
+  c->n_edge_dump = 0;
+  *block = b;
+  return 0;
+}
+
+void rgc_host_block_free(void* block) {
+  rgc_host_block* b = static_cast<rgc_host_block*>(block);
+  if (!b) return;
+  for (void* p : b->bufs) (void)hipHostFree(p);
+  delete b;
+}
+
 int rgc_kernel_times(rgc_ctx* c, int max_n, float* ms, const char** names) {
   if (!c) return fail("null ctx");
   const int n = std::min<int>(max_n, (int)c->times.size());

@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import weakref
 
 import numpy as np
 
@@ -82,6 +83,9 @@ lib.rgc_run.argtypes = [C.c_void_p, C.POINTER(BatchIn), C.POINTER(BatchOut)]
 lib.rgc_submit.argtypes = [C.c_void_p, C.POINTER(BatchIn)]
 lib.rgc_wait.argtypes = [C.c_void_p, C.POINTER(BatchOut)]
 lib.rgc_fetch_stats.argtypes = [C.c_void_p]
+lib.rgc_detach_host.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
+lib.rgc_host_block_free.argtypes = [C.c_void_p]
+lib.rgc_host_block_free.restype = None
 lib.rgc_last_edges.argtypes = [C.c_void_p, C.POINTER(_i32p), C.POINTER(_i32p),
                                C.POINTER(_f64p)]
 lib.rgc_last_edges.restype = C.c_int64
@@ -104,7 +108,7 @@ lib.rgc_pickle_bytes.argtypes = [C.POINTER(PickleFmt), C.POINTER(WriteIn), C.c_i
 lib.rgc_py_float_repr.argtypes = [C.c_double, C.c_char_p, C.c_int]
 
 EXPORTS = ["rgc_abi_version", "rgc_last_error", "rgc_device_count", "rgc_ctx_create",
-           "rgc_ctx_destroy", "rgc_run", "rgc_submit", "rgc_wait", "rgc_fetch_stats", "rgc_kernel_times", "rgc_last_edges", "rgc_parse_files",
+           "rgc_ctx_destroy", "rgc_run", "rgc_submit", "rgc_wait", "rgc_fetch_stats", "rgc_detach_host", "rgc_host_block_free", "rgc_kernel_times", "rgc_last_edges", "rgc_parse_files",
            "rgc_parsed_free", "rgc_py_hash_node", "rgc_py_set_order", "rgc_test_epilogue",
            "rgc_score_pairs", "rgc_ilp_solve", "rgc_write_outputs", "rgc_pickle_bytes",
            "rgc_py_float_repr"]
@@ -212,6 +216,32 @@ def device_count() -> int:
     return n.value
 
 
+class _HostLease:
+    """Owner of one run's host output buffers.  Every numpy view a :class:`Result` hands out
+    keeps it alive.  While the context still owns the buffers (``block`` None) nothing is
+    done; once the context moves on (next run, ILP / score call, close) while this lease is
+    still referenced, the context detaches the buffers into ``block`` (rgc_detach_host, ABI 7)
+    and they are freed here when the last view is gone."""
+
+    __slots__ = ("block", "__weakref__")
+
+    def __init__(self):
+        self.block = None
+
+    def view(self, p, ct, n):
+        """numpy view of n elements of ctypes type ct at address p, owned by this lease"""
+        ca = (ct * n).from_address(p)
+        ca._owner = self
+        return np.ctypeslib.as_array(ca)
+
+    def __del__(self):
+        if self.block:
+            try:
+                lib.rgc_host_block_free(self.block)
+            except Exception:  # noqa: BLE001 - interpreter shutdown
+                pass
+
+
 class Context:
     """One device + stream; owns the device workspace arena (grow-only)."""
 
@@ -220,9 +250,27 @@ class Context:
         _check(lib.rgc_ctx_create(int(device), C.c_void_p(stream or 0), C.byref(self._p)))
         self.device = device
         self._pending = None
+        self._lease = None   # weakref to the _HostLease of the last Result
+
+    def _retire(self):
+        """Before anything that may reuse or free the context's host buffers: if the last
+        Result (or any array taken from it) is still referenced, hand its buffers over to it."""
+        ref, self._lease = self._lease, None
+        lease = ref() if ref is not None else None
+        if lease is not None and lease.block is None and self._p:
+            h = C.c_void_p()
+            _check(lib.rgc_detach_host(self._p, C.byref(h)))
+            lease.block = h.value
+
+    def _result(self, bo, n_mg, k, flags, lazy_ctx=None):
+        lease = _HostLease()
+        self._lease = weakref.ref(lease)
+        return Result(bo, n_mg, k, flags, lazy_ctx, lease)
 
     def close(self):
         if self._p:
+            if self._pending is None:
+                self._retire()
             lib.rgc_ctx_destroy(self._p)
             self._p = C.c_void_p()
 
@@ -238,14 +286,15 @@ class Context:
         ``x``/``y``/``score`` are host float64 arrays, or device pointers (ints) with
         ``F_DEVICE_INPUTS``.  ``dev_meta`` = (device pointer of box_off as int32, device
         pointer of id_base) sets ``F_DEVICE_META``: the offsets are not uploaded per run.
-        Returns a :class:`Result` (views into context-owned memory that stay valid until the
-        next ``run``)."""
+        Returns a :class:`Result`; its host arrays stay valid as long as they are referenced
+        (rgc_detach_host hands them over when the context moves on)."""
         bi, keep, flags = self._batch_in(n_mg, k, box_size, box_off, id_base, x, y, score, flags,
                                          dev_meta)
+        self._retire()
         bo = BatchOut()
         _check(lib.rgc_run(self._p, C.byref(bi), C.byref(bo)))
         del keep
-        return Result(bo, n_mg, k, flags)
+        return self._result(bo, n_mg, k, flags)
 
     def submit(self, n_mg, k, box_size, box_off, id_base, x, y, score, flags=F_HOST_OUTPUTS,
                dev_meta=None):
@@ -255,6 +304,7 @@ class Context:
         batch i.  The arrays passed in must stay alive until ``wait`` (kept here)."""
         bi, keep, flags = self._batch_in(n_mg, k, box_size, box_off, id_base, x, y, score, flags,
                                          dev_meta)
+        self._retire()
         _check(lib.rgc_submit(self._p, C.byref(bi)))
         self._pending = (keep, n_mg, k, flags)
 
@@ -266,7 +316,7 @@ class Context:
         self._pending = None
         _check(lib.rgc_wait(self._p, C.byref(bo)))
         del keep
-        return Result(bo, n_mg, k, flags, self)
+        return self._result(bo, n_mg, k, flags, self)
 
     def _batch_in(self, n_mg, k, box_size, box_off, id_base, x, y, score, flags, dev_meta):
         # (kept lean: this runs once per batch inside the bench's timed region)
@@ -315,8 +365,11 @@ class Context:
 
 class Result:
     """Host view of one rgc_run.  Per-micrograph and per-clique arrays are numpy views of
-    context-owned pinned memory (per-clique arrays: device pointers without F_HOST_OUTPUTS);
-    like the C-ABI outputs they stay valid until the next ``run`` on the context."""
+    pinned memory (per-clique arrays: device pointers without F_HOST_OUTPUTS).  The host views
+    stay valid, with this run's values, for as long as they (or this Result) are referenced:
+    each holds the run's :class:`_HostLease`, and the context hands the buffers over to it
+    (rgc_detach_host) instead of reusing or freeing them.  Device pointers follow the C-ABI
+    rule: valid until the next run on the context."""
 
     _PER_MG = {"status": ("status", np.int32), "cc_max": ("cc_max", np.int32),
                "cc_cnt": ("cc_cnt", np.int32), "n_nodes": ("n_nodes", np.int32),
@@ -331,19 +384,23 @@ class Result:
         field, dt = spec
         dt = np.dtype(dt)
         if self._lazy is not None:   # F_LAZY_STATS: copied from HBM on first use
-            _check(lib.rgc_fetch_stats(self._lazy._p))
+            # (once the buffers were detached, rgc_detach_host has fetched them already)
+            if self._lease.block is None:
+                _check(lib.rgc_fetch_stats(self._lazy._p))
             self._lazy = None
         p = getattr(self._bo, field)
         if not self.n_mg or not p:
             v = np.zeros(0, dt)
         else:
             addr = C.cast(p, C.c_void_p).value
-            v = np.frombuffer((C.c_char * (self.n_mg * dt.itemsize)).from_address(addr), dt)
+            ct = {4: C.c_int32, 8: C.c_int64}[dt.itemsize]
+            v = self._lease.view(addr, ct, self.n_mg).view(dt)
         setattr(self, name, v)
         return v
 
-    def __init__(self, bo: BatchOut, n_mg: int, k: int, flags: int, ctx=None):
+    def __init__(self, bo: BatchOut, n_mg: int, k: int, flags: int, ctx=None, lease=None):
         self._bo = bo
+        self._lease = lease if lease is not None else _HostLease()
         self._lazy = ctx if (flags & F_LAZY_STATS) and ctx is not None else None
         self.n_mg, self.k = n_mg, k
         self.n_boxes, self.n_edges, self.n_cliques = bo.n_boxes, bo.n_edges, bo.n_cliques
@@ -352,7 +409,7 @@ class Result:
             def h(p, ct, n):
                 if not n or not p:
                     return np.zeros(n, dtype=np.dtype(ct))
-                return np.ctypeslib.as_array(C.cast(p, C.POINTER(ct)), shape=(n,))
+                return self._lease.view(C.cast(p, C.c_void_p).value, ct, n)
             self.rows = h(bo.rows, C.c_int32, C_ * k).reshape(C_, k)
             self.w = h(bo.w, C.c_float, C_)
             self.conf = h(bo.conf, C.c_float, C_)

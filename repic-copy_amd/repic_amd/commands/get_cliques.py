@@ -470,20 +470,20 @@ class _Run:
         # micrographs from the failing one on are removed (this shard's part of them)
         writer.close()
         if optimistic:
-            late = [mg.base for ch in done for i, mg in enumerate(ch.mgs)
-                    if ch.first + i >= gfail]
-            _remove_outputs(self.args.out_dir, late)
+            # exactly the files the writer wrote for those micrographs (Writer.written)
+            gi = {mg.base: ch.first + i for ch in done for i, mg in enumerate(ch.mgs)}
+            _remove_outputs(self.args.out_dir, [(b, sfx) for b, sfx in writer.written
+                                                if gi.get(b, -1) >= gfail])
         if fail == gfail:
             self.raise_for(stop_ch[1], stop_ch[0])
 
 
-def _remove_outputs(out_dir, bases):
-    """Remove what the writers produce for these micrographs (get_cliques.py:123-130,
-    215-229): the empty <base>.box of a skip or the four pickles and the runtime line."""
-    for b in bases:
-        for suf in (".box", "_weight_vector.pickle", "_consensus_coords.pickle",
-                    "_consensus_confidences.pickle", "_constraint_matrix.pickle",
-                    "_runtime.tsv"):
+def _remove_outputs(out_dir, written):
+    """Remove files this run wrote: ``written`` = (base, suffixes) pairs, the empty
+    <base>.box of a skip or the four pickles and the runtime.tsv of a micrograph with
+    cliques.  Nothing else in out_dir is touched (e.g. a run_ilp <base>.box)."""
+    for b, sufs in written:
+        for suf in sufs:
             try:
                 os.remove(os.path.join(out_dir, b + suf))
             except FileNotFoundError:

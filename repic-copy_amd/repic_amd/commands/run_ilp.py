@@ -6,7 +6,9 @@ Same plugin protocol and arguments as the reference module (repic/commands/run_i
 (:29-42,72-80), solves max w.x s.t. A x <= 1, x binary (:50-63) for every micrograph of the
 directory in one device batch (repic_amd.ilp), then writes what the reference writes, in its
 order: ``<base>.box`` (chosen cliques' consensus coordinates by decreasing confidence, rounded
-with np.rint, :112-124) and one more line of ``<base>_runtime.tsv`` (:127-131).
+with np.rint, :112-124) and one more line of ``<base>_runtime.tsv`` (:132-136, the seconds
+only, as the reference writes it).  The certification status and gap of each micrograph go to
+a sidecar ``<base>_ilp_status.tsv`` (``STATUS\tgap`` per run), which the reference lacks.
 
 Differences, stated: Gurobi stops at a 1e-4 relative MIP gap by default; this solver proves
 conflict components of up to 4096 cliques optimal exactly (f32 weights summed in f64) and
@@ -34,6 +36,8 @@ from ..ilp import solve_batch
 
 name = "run_ilp"
 
+# sidecar next to _runtime.tsv: one "STATUS\trelative_gap" line per run_ilp run
+STATUS_SUFFIX = "_ilp_status.tsv"
 STATUS_NAMES = {ilp.OPTIMAL: "OPTIMAL", ilp.GAP_OK: "GAP_OK", ilp.NODE_LIMIT: "NODE_LIMIT",
                 ilp.HEURISTIC: "HEURISTIC"}
 
@@ -122,9 +126,10 @@ def main(args):
                                         box_size, box_size, str(weight)]) + "\n")
         with open(out_file, "wt") as o:
             o.writelines(lines)
-        # run_ilp.py:132-136 appends the seconds; the certification status and the certified
-        # relative gap follow as two more columns, so an uncertified packing is visible
+        # run_ilp.py:132-136 appends the seconds, nothing else; the certification status and
+        # the certified relative gap go to a sidecar, so readers of _runtime.tsv are unchanged
         with open(mf.replace("_constraint_matrix.pickle", "_runtime.tsv"), "a") as o:
-            o.write(f"{share + time.time() - start}\t{STATUS_NAMES[status[i]]}\t"
-                    f"{rgap[i]:.3e}\n")
+            o.write(str(share + time.time() - start) + "\n")
+        with open(mf.replace("_constraint_matrix.pickle", STATUS_SUFFIX), "a") as o:
+            o.write(f"{STATUS_NAMES[status[i]]}\t{rgap[i]:.3e}\n")
     sys.stdout.flush()

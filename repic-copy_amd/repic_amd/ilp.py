@@ -77,6 +77,7 @@ def solve_batch(ctx, mats, weights, node_limit=0, timing=False, statuses=False, 
     gp = np.zeros(nc, np.float64)
     si = IlpIn(nc, n_rows, col_ptr.ctypes.data, row_idx.ctypes.data, w.ctypes.data,
                int(node_limit), _lib.F_TIMING if timing else 0, gp.ctypes.data)
+    ctx._retire()   # a live Result of an earlier run keeps its host buffers
     _lib._check(_lib.lib.rgc_ilp_solve(ctx._p, C.byref(si), x.ctypes.data, ex.ctypes.data))
     xs = [x[col_off[m]:col_off[m + 1]] for m in range(len(mats))]
     st, rel = [], []

@@ -130,6 +130,7 @@ def score_pairs(pairs, conf_thresh=None, mrc_w=None, mrc_h=None, ctx=None, timin
     counts = np.zeros((npairs, 3), dtype=np.int64)
     si = ScoreIn(npairs, H.ctypes.data, W.ctypes.data, gt_arr.ctypes.data, pk_arr.ctypes.data,
                  boxes.ctypes.data, _lib.F_TIMING if timing else 0)
+    ctx._retire()   # a live Result of an earlier run keeps its host buffers
     _lib._check(_lib.lib.rgc_score_pairs(ctx._p, C.byref(si), counts.ctypes.data))
     out = [_scores(counts[i], int(H[i]), int(W[i])) for i in range(npairs)]
     if timing:

@@ -241,6 +241,13 @@ def write_group(out_dir, items, w, conf, rows, cx, cy, cid):
         c0 = c1
 
 
+# the files written per micrograph (get_cliques.py:123-130, 215-229): the empty <base>.box
+# of a skip, or the four pickles and the runtime.tsv of a micrograph with cliques
+SKIP_FILES = (".box",)
+OK_FILES = ("_weight_vector.pickle", "_consensus_coords.pickle",
+            "_consensus_confidences.pickle", "_constraint_matrix.pickle", "_runtime.tsv")
+
+
 class Writer:
     """Pooled writer.  Pickling the per-micrograph objects holds the GIL, so large runs write
     from a pool of spawned processes (started early, chunks of ``chunk`` micrographs per
@@ -270,6 +277,8 @@ class Writer:
         self._futs = []
         self._bases = set()
         self._items = []
+        # (base, suffixes) of every file set handed to the pool, in submission order
+        self.written = []
         # optional timeline: ("write", first base, submit, done) seconds after t0, per group
         self.spans, self.t0 = None, 0.0
 
@@ -302,10 +311,12 @@ class Writer:
             f.result()
 
     def skip(self, out_dir, base):
+        self.written.append((base, SKIP_FILES))
         self._submit(0, (out_dir, base))
 
     def micrograph(self, out_dir, base, w, conf, rows, n_vert, cx, cy, cid, coords, seconds,
                    cc_max, cc_cnt):
+        self.written.append((base, OK_FILES))
         self._submit(1, (out_dir, base, w, conf, rows, n_vert, cx, cy, cid, coords, seconds,
                          cc_max, cc_cnt))
 
@@ -317,6 +328,7 @@ class Writer:
             self._flush()
             self._drain()
         self._bases.update(names)
+        self.written.extend((it[0], SKIP_FILES if it[1] < 0 else OK_FILES) for it in items)
         args = (out_dir, items, w, conf, rows, cx, cy, cid)
         t_sub = time.time()
         if self.native is not None and all(it[6] is None for it in items):

@@ -533,3 +533,72 @@ def test_gpu_cli_end_to_end_subprocess(tmp_path):
                         os.path.join(str(tmp_path), "out2"), str(meta2["box"])], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "ValueError" in r.stderr
+
+
+def test_gpu_result_views_outlive_next_run_and_close():
+    """Result arrays are views of pinned host memory the context owns; a Result still
+    referenced when the context moves on keeps its buffers (rgc_detach_host, ABI 7): a
+    coo_matrix built from ``r.rows`` reads the same values after a second, larger run (which
+    grows and would otherwise free or overwrite those buffers) and after ``close()``.  The
+    r04e segfault was this read after close (reference get_cliques.py:192-202 builds the COO
+    from the same rows)."""
+    from scipy.sparse import coo_matrix
+
+    from repic_amd import _lib, synth
+    from repic_amd.pipeline import Batch
+    cfg = synth.SynthConfig(**synth.CONFIGS["C2"], seed=3)
+    small = Batch.pack(cfg.k, cfg.box, synth.batch(cfg, 4))
+    big = Batch.pack(cfg.k, cfg.box, synth.batch(cfg, 400, start=4))
+    ctx = _lib.Context(0)
+    r = ctx.run(small.n_mg, cfg.k, cfg.box, small.box_off, small.id_base, small.x, small.y,
+                small.score, _lib.F_HOST_OUTPUTS)
+    C, V0 = int(r.clique_cnt[0]), int(r.n_vert[0])
+    b0 = int(r.clique_base[0])
+    rows = r.rows[b0:b0 + C].reshape(-1)
+    A = coo_matrix((np.ones(C * cfg.k, np.int64), (rows, np.repeat(np.arange(C), cfg.k))),
+                   shape=(V0, C))
+    want_rows, want_w, want_st = rows.copy(), r.w.copy(), r.status.copy()
+    r2 = ctx.run(big.n_mg, cfg.k, cfg.box, big.box_off, big.id_base, big.x, big.y, big.score,
+                 _lib.F_HOST_OUTPUTS)
+    assert int(r2.n_cliques) > 50 * int(r.n_cliques)       # the host buffers had to grow
+    assert (r.rows[b0:b0 + C].reshape(-1) == want_rows).all() and (r.w == want_w).all()
+    del r2
+    ctx.close()
+    assert (A.row == want_rows).all() and (A.tocsc().indices.size == C * cfg.k)
+    assert (r.status == want_st).all() and (r.w == want_w).all()
+    assert (A.toarray().sum(axis=0) == cfg.k).all()
+
+
+def test_gpu_lazy_stats_result_survives_next_submit():
+    """F_LAZY_STATS: a Result whose per-micrograph block was not fetched yet, still referenced
+    at the next submit on its context, gets its own run's stats (fetched at the hand-over),
+    not the newer run's (stale lazy stats)."""
+    import torch
+
+    from repic_amd import _lib, synth
+    from repic_amd.pipeline import Batch
+    cfg = synth.SynthConfig(**synth.CONFIGS["C2"], seed=5)
+    a = Batch.pack(cfg.k, cfg.box, synth.batch(cfg, 6))
+    b = Batch.pack(cfg.k, cfg.box, synth.batch(cfg, 9, start=6))
+    ctx = _lib.Context(0)
+    ref = ctx.run(a.n_mg, cfg.k, cfg.box, a.box_off, a.id_base, a.x, a.y, a.score, 0)
+    want = ref.clique_cnt.copy()
+    del ref
+    dev = []
+    for bt in (a, b):
+        dev.append([torch.from_numpy(v).cuda() for v in (bt.x, bt.y, bt.score)] +
+                   [torch.from_numpy(bt.box_off.astype(np.int32)).cuda(),
+                    torch.from_numpy(bt.id_base.astype(np.int64)).cuda()])
+    torch.cuda.synchronize()
+
+    def sub(bt, d):
+        ctx.submit(bt.n_mg, cfg.k, cfg.box, bt.box_off, bt.id_base, d[0].data_ptr(),
+                   d[1].data_ptr(), d[2].data_ptr(), _lib.F_DEVICE_INPUTS | _lib.F_LAZY_STATS,
+                   dev_meta=(d[3].data_ptr(), d[4].data_ptr()))
+    sub(a, dev[0])
+    ra = ctx.wait()
+    sub(b, dev[1])
+    rb = ctx.wait()
+    assert len(ra.clique_cnt) == a.n_mg and (ra.clique_cnt == want).all()
+    assert len(rb.clique_cnt) == b.n_mg
+    ctx.close()

@@ -21,7 +21,7 @@ from golden_util import load_case
 from repic_amd import _lib
 from repic_amd.commands import get_cliques as gc
 
-root, fail_at = sys.argv[1], int(sys.argv[2])
+root, fail_at, foreign = sys.argv[1], int(sys.argv[2]), sys.argv[3] == "1"
 meta, _ = load_case("c1_10017")
 args = argparse.Namespace(in_dir=os.path.join(root, "in"), out_dir=os.path.join(root, "out"),
                           box_size=meta["box"], multi_out=False, get_cc=False, threads=2,
@@ -35,6 +35,10 @@ class Res:
 
 def device(self, ch):
     time.sleep(0.3)                 # the writes of the previous chunk land meanwhile
+    if foreign:                     # files this run never writes (e.g. an earlier run_ilp's)
+        for mg in ch.mgs:
+            with open(os.path.join(self.args.out_dir, mg.base + "_runtime.tsv"), "w") as f:
+                f.write("foreign\n")
     st = np.full(max(1, len(ch.mgs)), _lib.OK, np.int32)
     for i, mg in enumerate(ch.mgs):
         if mg.status == "ok" and ch.first + i == fail_at:
@@ -61,7 +65,7 @@ dist.destroy_process_group()
 """
 
 
-def _run(tmp_path, fail_at):
+def _run(tmp_path, fail_at, foreign=False):
     from golden_util import make_inputs
     make_inputs("c1_10017", str(tmp_path))
     port = _free_port()
@@ -71,7 +75,8 @@ def _run(tmp_path, fail_at):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RGC_CLI_GLOO="1",
                    PYTHONPATH=os.pathsep.join([ROOT, os.path.join(ROOT, "repic-copy_amd"),
                                                os.path.join(ROOT, "tests")]))
-        procs.append(subprocess.Popen([sys.executable, "-c", CODE, str(tmp_path), str(fail_at)],
+        procs.append(subprocess.Popen([sys.executable, "-c", CODE, str(tmp_path), str(fail_at),
+                                       "1" if foreign else "0"],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                                       text=True))
     out = []
@@ -115,3 +120,21 @@ def test_sharded_stream_failure_removes_later_files(tmp_path, fail_at):
     names = _names()
     written = sorted(f[:-4] for f in os.listdir(tmp_path / "out") if f.endswith(".box"))
     assert written == sorted(names[:fail_at])
+
+
+@pytest.mark.timeout(300)
+def test_sharded_failure_cleanup_removes_only_written_files(tmp_path):
+    """the cleanup after a failure removes only the files the writer wrote for the
+    micrographs from the failing one on (here each one's empty .box), never other files of
+    those names (here a <base>_runtime.tsv the run did not write)."""
+    fail_at = 3
+    res = _run(tmp_path, fail_at, foreign=True)
+    assert [r["exc"] for r in res].count("ValueError") == 1
+    names = _names()
+    out = tmp_path / "out"
+    assert sorted(f[:-4] for f in os.listdir(out) if f.endswith(".box")) == sorted(names[:fail_at])
+    # every chunk the device saw created a foreign runtime.tsv; none of them was removed
+    kept = {f[:-len("_runtime.tsv")] for f in os.listdir(out) if f.endswith("_runtime.tsv")}
+    assert set(names[fail_at:]) & kept, kept
+    for b in kept:
+        assert open(out / (b + "_runtime.tsv")).read() == "foreign\n"
