@@ -30,6 +30,11 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 DEFAULT_MG = {"C2": 10000, "C3": 4000, "C4": 12500, "C5": 64}
+# by_config entries: name -> (BASELINE config, micrographs per GPU).  C4_100k is the north-star
+# batch (BASELINE configs[3]: 100k micrographs, 5 pickers) on ONE GPU, the 1-GPU point of the
+# 1 -> 8 curve; C4 is its 12.5k-micrograph per-GPU shard at 8 GPUs.
+BY_CONFIG = {"C2": ("C2", 10000), "C3": ("C3", 4000), "C4": ("C4", 12500), "C5": ("C5", 64),
+             "C4_100k": ("C4", 100000)}
 
 
 def fused_compulsory_bytes(N, C, k, V, n_mg):
@@ -324,7 +329,8 @@ class Env:
         self.cdev = self.dev if self.backend == "nccl" else torch.device("cpu")
 
 
-def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=False):
+def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=False,
+            lazy_stats=True):
     """Time ``steps`` steps of the hot path over one synthetic batch of ``config`` (n_mg
     micrographs per rank, inputs resident in HBM): barrier + synchronize on both sides, max
     over ranks.  Returns (report dict, cfg, this rank's micrographs)."""
@@ -336,8 +342,13 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
     dist, world, rank, dev, cdev = env.dist, env.world, env.rank, env.dev, env.cdev
     cfg = synth.SynthConfig(**synth.CONFIGS[config], seed=args.seed)
     t_gen = time.time()
-    mgs = synth.batch(cfg, n_mg, start=rank * n_mg)    # this rank's shard of one big batch
-    batch = Batch.pack(cfg.k, cfg.box, mgs)
+    # this rank's shard of one big batch (identical to packing synth.batch's list; large
+    # batches are generated by a process pool)
+    procs = min(16, len(os.sched_getaffinity(0))) if n_mg * cfg.n_true * cfg.k >= 2_000_000 else 1
+    batch = Batch.from_counts(cfg.k, cfg.box, *synth.packed(cfg, n_mg, start=rank * n_mg,
+                                                             procs=procs))
+    # the first micrographs as per-picker arrays, for the CPU baseline's sample
+    mgs = synth.batch(cfg, min(n_mg, 64 if config != "C3" else 8), start=rank * n_mg)
     t_gen = time.time() - t_gen
     # the one exchange of the sharded path: global box-id offsets
     if dist is not None:
@@ -385,7 +396,8 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
         # the run's totals; the last step's stats are fetched after the timed region)
         c.submit(batch.n_mg, cfg.k, cfg.box, batch.box_off, batch.id_base,
                  dx.data_ptr(), dy.data_ptr(), ds.data_ptr(),
-                 flags | _lib.F_LAZY_STATS | (_lib.F_TIMING if timing else 0),
+                 flags | (_lib.F_LAZY_STATS if lazy_stats else 0) |
+                 (_lib.F_TIMING if timing else 0),
                  dev_meta=(dbo.data_ptr(), did.data_ptr()))
 
     def steps_run(n, timing, ktimes=None):
@@ -500,7 +512,7 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
                      "achieved_gbs": pipe / (dev_ms * 1e-3) / 1e9,
                      "frac": pipe / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "kernel_ms": {k_: round(v, 4) for k_, v in sorted(avg.items())}},
-        "gen_s": t_gen,
+        "gen_s": t_gen, "gen_procs": procs,
     }
     return out, cfg, mgs
 
@@ -537,9 +549,11 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="synchronous rgc_run per step instead of two contexts in flight")
     ap.add_argument("--by-config", default=None,
-                    help="comma-separated configs also timed in this run and reported under "
-                         "by_config (default: every other BASELINE config at its bench size, "
-                         "when --n_mg is not given; 'none' to skip)")
+                    help="comma-separated by_config entries (BY_CONFIG names) also timed in this "
+                         "run (default: every other BASELINE config at its bench size plus "
+                         "C4_100k, when --n_mg is not given; 'none' to skip)")
+    ap.add_argument("--by-config-cpu-budget", type=float, default=6.0,
+                    help="seconds of the 1-core CPU baseline sample per by_config entry (0: none)")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -560,29 +574,78 @@ def main():
     out = {"metric": "micrographs/sec (get_cliques, whole node) at 1/2/4/8 MI355X; % HBM roofline"}
     out.update(rep)
     out.update({"higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-                "dtype": "f64", "data": "synthetic (seeded SURVEY.md §8(d) generator)"})
+                "dtype": "f64", "data": "synthetic (seeded SURVEY.md §8(d) generator)",
+                "stats_copy": "per-micrograph stats stay in HBM during the timed steps "
+                              "(RGC_F_LAZY_STATS, since round 4): each step copies its 128-B "
+                              "cursor block; see stats_copy_variant for the rate with every "
+                              "step's per-micrograph stats copied to the host"})
     # the other BASELINE configs in the same run (same steps / warmup, their bench sizes:
-    # C4 at the 100k / 8-GPU shard of 12.5k micrographs per GPU); the CPU baseline stays on
-    # the headline config
+    # C4 at the 100k / 8-GPU shard of 12.5k micrographs per GPU, C4_100k the whole north-star
+    # batch on this GPU), each with a 1-core CPU baseline sample on rank 0
     if args.by_config is None:
-        extra = [] if args.n_mg else [c for c in ("C2", "C3", "C4", "C5") if c != args.config]
+        extra = [] if args.n_mg else [c for c in ("C2", "C3", "C4", "C5", "C4_100k")
+                                      if c != args.config]
     elif args.by_config.lower() == "none":
         extra = []
     else:
         extra = [c.strip() for c in args.by_config.split(",") if c.strip()]
+    cpu_rank0 = env.rank == 0 and world == 1
     if extra and not args.host_io:
         byc = {args.config: by_config_entry(rep)}
-        for c in extra:
-            r_c, _, _ = measure(args, env, c, DEFAULT_MG[c], args.steps, args.warmup,
-                                no_pipeline=args.no_pipeline)
-            byc[c] = by_config_entry(r_c)
+        cpu_of = {}
+        for name in extra:
+            config, n_c = BY_CONFIG[name]
+            r_c, cfg_c, mgs_c = measure(args, env, config, n_c, args.steps, args.warmup,
+                                        no_pipeline=args.no_pipeline)
+            byc[name] = by_config_entry(r_c)
+            if cpu_rank0 and args.by_config_cpu_budget > 0 and not args.no_cpu_baseline:
+                if config not in cpu_of:
+                    cpu_of[config] = cpu_baseline(cfg_c, mgs_c, args.by_config_cpu_budget,
+                                                  procs=1, config=config)
+                cb = dict(cpu_of[config])
+                if n_c >= 50000:
+                    cb["glob_pairing"] = glob_pairing_term(n_c, cfg_c.k)
+                byc[name]["cpu_baseline"] = cb
         out["by_config"] = byc
-    if env.rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if cpu_rank0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, mgs, args.cpu_budget, config=args.config)
+        if "by_config" in out:
+            out["by_config"][args.config]["cpu_baseline"] = out["cpu_baseline"]
+    if not args.host_io and not args.no_pipeline and n_mg == DEFAULT_MG.get(args.config):
+        # the rate with every step's per-micrograph stats copied to the host (what
+        # the CLI reads), next to the headline's lazy-stats rate
+        r_s, _, _ = measure(args, env, args.config, n_mg, args.steps, args.warmup,
+                            lazy_stats=False)
+        out["stats_copy_variant"] = {"value": r_s["value"], "ms_per_step": r_s["ms_per_step"],
+                                     "note": "same workload, per-micrograph stats (48 B each) "
+                                             "copied to pinned host memory in every step"}
     if env.rank == 0:
         print(json.dumps(out), flush=True)
     if env.dist is not None:
         env.dist.destroy_process_group()
+
+
+def glob_pairing_term(n_mg, k, sample=20000):
+    """BASELINE.md §3 for C4 at 100k: the reference pairs each micrograph with its partner
+    files by ``glob(in/methods[p]/*{base}*)`` (get_cliques.py:94,121), a scan of the whole
+    picker directory per call: M (k - 1) calls of O(M) each.  Timed here on a directory of
+    ``sample`` empty files named like the synthetic ones, scaled linearly to M files; the
+    CPU baseline's per-micrograph rate above excludes it."""
+    import glob
+    import tempfile
+    with tempfile.TemporaryDirectory(dir="/tmp") as d:
+        for i in range(sample):
+            open(os.path.join(d, f"mg{i:06d}.box"), "w").close()
+        t0 = time.perf_counter()
+        reps = 5
+        for r in range(reps):
+            assert len(glob.glob(os.path.join(d, f"*mg{(r * 3571) % sample:06d}*"))) == 1
+        per = (time.perf_counter() - t0) / reps
+    per_m = per * n_mg / sample
+    return {"seconds_per_glob_at_M": per_m, "calls": n_mg * (k - 1),
+            "total_hours": per_m * n_mg * (k - 1) / 3600.0,
+            "sample": f"glob over a directory of {sample} files: {per * 1e3:.2f} ms per call, "
+                      f"scaled linearly to {n_mg} files; not part of the CPU rate"}
 
 
 if __name__ == "__main__":

@@ -43,6 +43,17 @@ class Batch:
                          if len(counts) else np.zeros(0))
         return cls(k, box_size, box_off, id_bases, cat(0), cat(1), cat(2))
 
+    @classmethod
+    def from_counts(cls, k, box_size, counts, x, y, score):
+        """From per-(micrograph, picker) box counts and the concatenated arrays (synth.packed);
+        id bases as in ``pack``."""
+        counts = np.asarray(counts, np.int64)
+        box_off = np.zeros(len(counts) + 1, np.int64)
+        np.cumsum(counts, out=box_off[1:])
+        per_mg = counts.reshape(-1, k).sum(axis=1)
+        id_bases = np.concatenate([[0], np.cumsum(per_mg)[:-1]]) if len(per_mg) else per_mg
+        return cls(k, box_size, box_off, id_bases, x, y, score)
+
     def slice(self, m0, m1):
         k = self.k
         b0, b1 = int(self.box_off[m0 * k]), int(self.box_off[m1 * k])

@@ -8,9 +8,13 @@ reads exactly 1/2 of a wide (16 B/lane) coalesced streaming read on gfx950; our 
 4-8 B per lane in gathers, a width the guide leaves uncalibrated, so the fetch side is
 reported raw (x1024) and flagged, not doubled.
 
-SQ_* counters are in quad-cycles (guide: "SQ_WAVE_CYCLES/SQ_WAIT_*/SQ_ACTIVE_INST_* count
-quad-cycles"); GRBM_GUI_ACTIVE is summed over the 8 XCDs.  Derived per kernel:
-  valu_busy  = 4 * SQ_ACTIVE_INST_VALU / (GRBM_GUI_ACTIVE / 8 * 1024 SIMDs)
+SQ_WAVE_CYCLES / SQ_WAIT_* count quad-cycles (guide); SQ_ACTIVE_INST_VALU does NOT: on gfx950
+it equals SQ_INSTS_VALU, an instruction count, and a wave64 VALU instruction takes 2 SIMD
+cycles when >= 2 waves per SIMD are ready (calibrated by tools/probe/valu_cal.hip,
+profiles/r05a_valu_calibration.json: the saturated 8-waves/SIMD probe reads 0.85 with the
+factor 2 and an impossible 1.70 with the factor 4 used until round 4).  GRBM_GUI_ACTIVE is
+summed over the 8 XCDs.  Derived per kernel:
+  valu_busy  = 2 * SQ_ACTIVE_INST_VALU / (GRBM_GUI_ACTIVE / 8 * 1024 SIMDs)
   wait_any   = SQ_WAIT_ANY / SQ_WAVE_CYCLES          (share of resident wave time stalled)
   waves_per_cu = 4 * SQ_WAVE_CYCLES / (GRBM_GUI_ACTIVE / 8 * 256 CUs)
   lane_eff   = SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU)   (when collected)
@@ -35,6 +39,7 @@ NAMES = [(r"k5_cliques<\d+, true>", "k5_cliques_fill"), (r"k5_cliques<\d+, false
          (r"k_fused<", "k_fused"), (r"k7_rows<", "k7_rows"), (r"rgc::(k\w+)", None),
          (r"rgc::(scan_\w+)\(", None)]
 N_XCD, N_CU, N_SIMD = 8, 256, 1024
+VALU_CYCLES = 2     # SIMD cycles per wave64 VALU instruction (profiles/r05a_valu_calibration.json)
 
 
 def event_name(kname):
@@ -64,7 +69,7 @@ def derive(c):
     if g:
         per_xcd = g / N_XCD
         if "SQ_ACTIVE_INST_VALU" in c:
-            out["valu_busy"] = 4 * c["SQ_ACTIVE_INST_VALU"] / (per_xcd * N_SIMD)
+            out["valu_busy"] = VALU_CYCLES * c["SQ_ACTIVE_INST_VALU"] / (per_xcd * N_SIMD)
         if "SQ_WAVE_CYCLES" in c:
             out["waves_per_cu"] = 4 * c["SQ_WAVE_CYCLES"] / (per_xcd * N_CU)
     if c.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in c:
