@@ -235,6 +235,9 @@ static int ensure_dev(rgc_ctx* c, int id, size_t bytes, size_t keep = 0) {
   if (b.p) HIPCHK(hipFree(b.p));
   b.p = p;
   b.cap = cap;
+  // the scan tile buffer's word 0 is the one-pass scan's claim counter: zero in a new buffer
+  // (every scan leaves it zero)
+  if (id == D_TILES) HIPCHK(hipMemsetAsync(p, 0, 64, c->stream));
   return 0;
 }
 

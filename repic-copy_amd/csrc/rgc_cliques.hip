@@ -600,8 +600,12 @@ __device__ __forceinline__ uint64_t spread_even(uint64_t v) {
 // Same arithmetic as the fused kernel's epilogue (rgc_fused.hip fused_epilogue_main / _order).
 // Thread t takes cliques 2t and 2t + 1: the packed-u16 pair path when both qualify, one at a
 // time otherwise.
+#ifndef RGC_EPI_WPE_N
+#define RGC_EPI_WPE_N 3
+#endif
+#define RGC_EPI_WPE __attribute__((amdgpu_waves_per_eu(RGC_EPI_WPE_N)))
 template <int K>
-__global__ __launch_bounds__(WG) void k5_epilogue(CliqueArgs A) {
+__global__ __launch_bounds__(WG) RGC_EPI_WPE void k5_epilogue(CliqueArgs A) {
   const int64_t j0 = 2 * ((int64_t)blockIdx.x * WG + threadIdx.x);
   if (j0 >= A.C) return;
   const bool two = j0 + 1 < A.C;

@@ -1233,6 +1233,10 @@ void k_fused(FusedArgs A) {
   } while (0)
 #endif
   STAMP(0);
+#ifdef RGC_STAMPS
+  // workgroup timeline (s_memrealtime, 100 MHz, chip-wide): start in the low half of slot 13
+  const uint32_t rt0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
   FCtx<K> c;
   c.B = sdetach(A.B); c.two_b2 = sdetach(A.two_b2); c.flags = sdetach(A.flags);
   c.score = gdetach(A.score);
@@ -1868,6 +1872,7 @@ void k_fused(FusedArgs A) {
         if (S.flags[t] == 3) c.S.vscore[S.vrank[t]] = c.score[b0 + S.citems[t]];
       __syncthreads();
     }
+
     STAMP(11);  // score staging
     // per chunk of queued cliques: main pass (thread per clique), then the order pass over
     // the cliques it flagged (bit 15 of the slot's ordinal word; the slot's output index is
@@ -1980,6 +1985,11 @@ void k_fused(FusedArgs A) {
     }   // !overflow
   }
   STAMP(12);
+#ifdef RGC_STAMPS
+  if (tid == 0)
+    A.stamps[(int64_t)blockIdx.x * 16 + 13] =
+        ((unsigned long long)(uint32_t)__builtin_amdgcn_s_memrealtime() << 32) | rt0;
+#endif
   if constexpr (QG) {
     if (qslot >= 0) {   // every thread is done with the slot
       __syncthreads();

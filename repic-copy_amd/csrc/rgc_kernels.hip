@@ -24,6 +24,8 @@
 #include "rgc_device.h"
 #include "rgc_kernels.h"
 
+#include <atomic>
+
 namespace rgc {
 
 // ----------------------------------------------------------------------------- K1 bin
@@ -363,6 +365,114 @@ __global__ __launch_bounds__(WG) void scan_apply(int64_t n, const int32_t* __res
     pre += v[i];
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = *total;
+}
+
+// Single-pass exclusive scan (decoupled look-back): one launch instead of scan_tiles +
+// scan_sums + scan_apply, reading the counts once and writing the offsets once.  Tiles of
+// ONE_TILE counts are claimed in order on a counter (a tile's predecessors are then already
+// running or done, whatever the dispatch order); each tile publishes its aggregate, looks back
+// over its predecessors' published states (one wave, 64 states per step) for the exclusive
+// prefix, then publishes its inclusive prefix.  A tile state is one 64-bit word: flag (2 bits:
+// 1 aggregate, 2 inclusive prefix), launch epoch (22 bits: states of earlier launches read as
+// unpublished, so the array needs no clearing) and value (40 bits).  The launch's last claim
+// zeroes the counter for the next launch.  Counter and states live in the caller's tile buffer:
+// word 0 the counter (zero when the buffer is new), states from word 1.
+constexpr int ONE_PER = 16;
+constexpr int ONE_TILE = WG * ONE_PER;
+constexpr uint64_t ST_AGG = 1ull << 62, ST_INC = 2ull << 62;
+constexpr uint64_t ST_VAL = (1ull << 40) - 1;
+
+__device__ __forceinline__ uint64_t ep_mask() { return ((1ull << 22) - 1) << 40; }
+__device__ __forceinline__ uint64_t st_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(WG) void scan_onepass(int64_t n, const int32_t* __restrict__ in,
+                                                   int64_t* __restrict__ out, int64_t* total,
+                                                   uint64_t* buf, uint32_t epoch) {
+  __shared__ int64_t red[NW];
+  __shared__ int64_t s_pre;
+  __shared__ uint32_t s_tile;
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(buf);
+  uint64_t* state = buf + 1;
+  const uint64_t ep = (uint64_t)epoch << 40;
+  const int ntiles = (int)gridDim.x;
+  if (threadIdx.x == 0) {
+    int vz;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(vz));   // (keeps the atomic optimizer off it)
+    const uint32_t t = atomicAdd(ctr + vz, 1u);
+    if (t == (uint32_t)ntiles - 1u) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_tile = t;
+  }
+  __syncthreads();
+  const int tile = (int)s_tile;
+  const int64_t t0 = (int64_t)tile * ONE_TILE + (int64_t)threadIdx.x * ONE_PER;
+  int32_t v[ONE_PER];
+  const bool vec = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+  if (vec && t0 + ONE_PER <= n) {
+    const int4* q = reinterpret_cast<const int4*>(in + t0);
+#pragma unroll
+    for (int i = 0; i < ONE_PER / 4; ++i) {
+      const int4 w = q[i];
+      v[4 * i] = w.x; v[4 * i + 1] = w.y; v[4 * i + 2] = w.z; v[4 * i + 3] = w.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < ONE_PER; ++i) v[i] = t0 + i < n ? in[t0 + i] : 0;
+  }
+  int64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < ONE_PER; ++i) s += v[i];
+  int64_t agg;
+  int64_t pre = block_excl_scan(s, red, &agg);
+  if (threadIdx.x < 64) {   // wave 0: publish, look back, publish the inclusive prefix
+    const int lane = threadIdx.x;
+    if (lane == 0) st_store(state + tile, (tile == 0 ? ST_INC : ST_AGG) | ep | (uint64_t)agg);
+    int64_t excl = 0;
+    int j = tile - 1;   // the highest predecessor not yet folded in
+    for (int guard = 0; j >= 0 && guard < (1 << 24); ++guard) {
+      const int idx = j - lane;
+      uint64_t w = idx >= 0 ? st_load(state + idx) : (ST_INC | ep);   // (before tile 0: 0)
+      const bool ready = (w & ep_mask()) == ep && (w >> 62) != 0;
+      if (__ballot(!ready)) continue;   // some state of this window is not published yet
+      const uint64_t inc = __ballot((w >> 62) == 2);
+      // lanes up to and including the first inclusive one (lowest lane = highest tile)
+      const int first = inc ? __builtin_ctzll(inc) : 64;
+      int64_t val = (lane <= first && idx >= 0) ? (int64_t)(w & ST_VAL) : 0;
+      for (int o = 32; o > 0; o >>= 1) val += __shfl_xor(val, o, 64);
+      excl += val;
+      if (inc) break;
+      j -= 64;
+    }
+    if (lane == 0) {
+      if (tile > 0) st_store(state + tile, ST_INC | ep | (uint64_t)(excl + agg));
+      s_pre = excl;
+      if (tile == ntiles - 1) {
+        out[n] = excl + agg;
+        *total = excl + agg;
+      }
+    }
+  }
+  __syncthreads();
+  pre += s_pre;
+  if (vec && t0 + ONE_PER <= n) {
+#pragma unroll
+    for (int i = 0; i < ONE_PER; i += 2) {
+      const int64_t a = pre;
+      pre += v[i];
+      reinterpret_cast<longlong2*>(out + t0)[i / 2] = make_longlong2(a, pre);
+      pre += v[i + 1];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < ONE_PER; ++i) {
+      if (t0 + i < n) out[t0 + i] = pre;
+      pre += v[i];
+    }
+  }
 }
 
 // ----------------------------------------------------------------------------- K4 CC
@@ -834,15 +944,25 @@ void launch_pairs(hipStream_t stream, bool fill, int N, int k, double B, double 
                sx, sy, sbox, spick, smg, fwd_cnt, fwd_off, e_dst, e_ji);
 }
 
-int64_t scan_tiles_needed(int64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 1; }
+// tile buffer words: the one-pass scan's claim counter + one state per tile (the three-launch
+// scan's tile sums fit the same words)
+int64_t scan_tiles_needed(int64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 2; }
 
 void launch_scan(hipStream_t stream, int64_t n, const int32_t* in, int64_t* out,
                  int64_t* tile_buf, int64_t* total) {
+#ifdef RGC_X_SCAN3   // the three-launch scan (A/B timing)
   const int64_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
-  if (nt > 0) RGC_LAUNCH(scan_tiles, nt, WG, n, in, tile_buf);
-  RGC_LAUNCH(scan_sums, 1, 1024, nt, tile_buf, total);
-  if (nt > 0) RGC_LAUNCH(scan_apply, nt, WG, n, in, tile_buf, total, out);
+  if (nt > 0) RGC_LAUNCH(scan_tiles, nt, WG, n, in, tile_buf + 1);
+  RGC_LAUNCH(scan_sums, 1, 1024, nt, tile_buf + 1, total);
+  if (nt > 0) RGC_LAUNCH(scan_apply, nt, WG, n, in, tile_buf + 1, total, out);
   else (void)hipMemcpyAsync(out, total, sizeof(int64_t), hipMemcpyDeviceToDevice, stream);
+#else
+  // launch epochs are process-wide (any two launches sharing a tile buffer differ)
+  static std::atomic<uint32_t> epochs{0};
+  const uint32_t e = epochs.fetch_add(1) % ((1u << 22) - 1) + 1;
+  const int64_t nt = std::max<int64_t>(1, (n + ONE_TILE - 1) / ONE_TILE);
+  RGC_LAUNCH(scan_onepass, nt, WG, n, in, out, total, reinterpret_cast<uint64_t*>(tile_buf), e);
+#endif
 }
 
 void launch_cc(hipStream_t stream, int phase, int N, int n_mg, int k, int get_cc,

@@ -1,13 +1,16 @@
 #!/bin/bash
-# Per-phase stamps (diagnostic build) for the given configs.
-#   gpurun --timeout 300 -- bash tools/gpu_stamps.sh TAG "C2:10000 C4:4000"
+# Per-phase s_memtime shares and the workgroup timeline of the fused kernel (diagnostic build
+# librepic_gc_diag.so, built on the CPU side with `make -C repic-copy_amd/csrc diag`).
+#   gpurun --timeout 300 -- bash tools/gpu_stamps.sh TAG [CONFIG:N_MG ...]
 set -e -o pipefail
-TAG=${1:-stamps}; CFGS=${2:-"C2:10000 C4:4000"}
+TAG=${1:-stamps}
+shift || true
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
+CFGS=${*:-C2:10000}
 for cn in $CFGS; do
   C=${cn%%:*}; N=${cn##*:}
-  REPIC_GC_LIB=repic-copy_amd/repic_amd/librepic_gc_diag.so timeout -k 10 200 \
-    python -u tools/phase_stamps.py $C $N > "$OUT/stamps_$C.txt" 2>&1 || { tail -20 "$OUT/stamps_$C.txt"; exit 1; }
+  timeout -k 10 120 python -u tools/phase_stamps.py "$C" "$N" > "$OUT/stamps_$C.txt" 2>&1 \
+    || { tail -20 "$OUT/stamps_$C.txt"; exit 1; }
   cat "$OUT/stamps_$C.txt"
 done

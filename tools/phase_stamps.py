@@ -52,3 +52,26 @@ for i, nm in enumerate(names):
 print(f"  per-WG total cycles: mean {tot.mean():.0f} p50 {np.median(tot):.0f} p99 {np.percentile(tot, 99):.0f}")
 span = st[valid, 12].max() - st[valid, 0].min()
 print(f"  launch span {span} cycles; sum(WG cycles)/span = {tot.sum() / span:.1f} concurrent WGs")
+
+# workgroup timeline from s_memrealtime (slot 13: end << 32 | start, 100 MHz): concurrency over
+# the launch and the tail (time while fewer than 90 % of the peak workgroups are resident)
+rt = raw[valid, 13].astype(np.uint64)
+t0 = (rt & np.uint64(0xFFFFFFFF)).astype(np.int64)
+t1 = (rt >> np.uint64(32)).astype(np.int64)
+t1 = np.where(t1 < t0, t1 + (1 << 32), t1)
+base = t0.min()
+t0, t1 = t0 - base, t1 - base
+ev = np.concatenate([np.stack([t0, np.ones_like(t0)], 1), np.stack([t1, -np.ones_like(t1)], 1)])
+ev = ev[np.lexsort((ev[:, 1], ev[:, 0]))]
+conc = np.cumsum(ev[:, 1])
+tt = ev[:, 0]
+peak = conc.max()
+dur = (t1.max()) * 10e-3   # us
+wg_us = (t1 - t0) * 10e-3
+below = tt[conc >= 0.9 * peak]
+tail = (t1.max() - below.max()) * 10e-3 if len(below) else 0.0
+ramp = below.min() * 10e-3 if len(below) else 0.0
+area = np.sum(np.diff(tt) * conc[:-1]) * 10e-3
+print(f"  timeline: span {dur:.1f} us, peak {peak} resident WGs, mean {area / dur:.0f}; "
+      f"WG time mean {wg_us.mean():.1f} us p50 {np.median(wg_us):.1f} p99 {np.percentile(wg_us, 99):.1f}; "
+      f"ramp to 90% {ramp:.1f} us, tail below 90% {tail:.1f} us")
