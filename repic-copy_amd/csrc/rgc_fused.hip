@@ -630,11 +630,28 @@ __device__ __forceinline__ float bfs_fit(int64_t need, int64_t have) {
 // then, so first segments come from a binary search for the next picker's first position and
 // a root is valid iff it was marked as a clique vertex in P4 (it has a clique, which lies in
 // the --get_cc target component); vertices are already marked.
-template <int K, int D, int NT>
+// WE (wide entries, K <= 4, the HBM level-tree slot of the QG launches): an entry holds its
+// prefix's members themselves (four u16 in 8 bytes) instead of (parent index, last member), so
+// reading a prefix is one load instead of a chain of D - 1 dependent ones (L2 latency each).
+template <bool WE>
+constexpr int bfs_es() { return WE ? 8 : 4; }
+__device__ __forceinline__ uint2 we_pack(const int (&mm)[4], int d, int h) {
+  int t[4] = {mm[0], mm[1], mm[2], mm[3]};
+  t[d] = h;
+  return make_uint2((uint32_t)t[0] | ((uint32_t)t[1] << 16), (uint32_t)t[2] | ((uint32_t)t[3] << 16));
+}
+template <int K, int D, int NT, bool WE = false>
 struct BfsLevel {
   // prefix members of entry e of level D (D members, compile-time indices only)
   __device__ __forceinline__ static void prefix(const char* q, const int (&lvl)[K + 1],
                                                 uint32_t e, int (&mm)[K]) {
+    if constexpr (WE) {
+      const uint2 v = reinterpret_cast<const uint2*>(q + lvl[D])[e];
+      const int t[4] = {(int)(v.x & 0xFFFF), (int)(v.x >> 16), (int)(v.y & 0xFFFF), (int)(v.y >> 16)};
+#pragma unroll
+      for (int d = 0; d < D; ++d) mm[d] = t[d];
+      return;
+    }
     uint32_t ent = reinterpret_cast<const uint32_t*>(q + lvl[D])[e];
     mm[D - 1] = (int)(ent & 0xFFFF);
     uint32_t cur = ent >> 16;
@@ -658,13 +675,14 @@ struct BfsLevel {
                                                   int qbytes, BfsOut<K>& out, int64_t nD, int tid,
                                                   const int (&pp)[K + 1]) {
     int (&lvl)[K + 1] = out.lvl;
+    constexpr int ES = bfs_es<WE>();
     // temps of this level at the top of q
     const int tb = (qbytes - 8 * (int)(nD + 1)) & ~7;
     if (K >= 4) {   // (K = 3 runs one attempt: no chunk sizing)
-      const float f = fminf(bfs_fit(nD, 65535), bfs_fit(12 * nD, qbytes - lvl[D] - 8));
+      const float f = fminf(bfs_fit(nD, 65535), bfs_fit((8 + ES) * nD, qbytes - lvl[D] - 8));
       out.fit = fminf(out.fit, f);
     }
-    if (nD > 65535 || tb < lvl[D] + 4 * (int)nD) {
+    if (nD > 65535 || tb < lvl[D] + ES * (int)nD) {
       out.C = -1;
       out.fit = fminf(out.fit, 0.999f);
       return out;
@@ -698,12 +716,12 @@ struct BfsLevel {
     // (32-bit scan: nD <= 65535 entries of at most n <= 4608 extensions each, < 2^31)
     const int64_t nN = ufl(block_scan_dpp32<NT>(CN, (int)nD, H.redi));
     constexpr bool last = D + 1 == K;
-    const int nb = ufl((lvl[D] + 4 * (int)nD + 3) & ~3);   // next level starts here
+    const int nb = ufl((lvl[D] + ES * (int)nD + 7) & ~7);   // next level starts here
     if (K >= 4) {
-      const float f = fminf(bfs_fit(nN, 65535), bfs_fit(nN * (last ? 6 : 4), tb - nb));
+      const float f = fminf(bfs_fit(nN, 65535), bfs_fit(nN * (last ? ES + 2 : ES), tb - nb));
       out.fit = fminf(out.fit, f);
     }
-    if (nN > 65535 || nN * (last ? 6 : 4) > tb - nb) {
+    if (nN > 65535 || nN * (last ? ES + 2 : ES) > tb - nb) {
       out.C = -1;
       out.fit = fminf(out.fit, 0.999f);
       return out;
@@ -727,14 +745,21 @@ struct BfsLevel {
             ok = ok && contains16(S.dst, S.fwd[mm[d]], S.fwd[mm[d] + 1], h);
         }
         if (!ok) continue;
-        reinterpret_cast<uint32_t*>(q + nb)[o] = ((uint32_t)e << 16) | (uint32_t)h;
+        if constexpr (WE) {
+          int m4[4] = {0, 0, 0, 0};
+#pragma unroll
+          for (int d = 0; d < D && d < 4; ++d) m4[d] = mm[d];
+          reinterpret_cast<uint2*>(q + nb)[o] = we_pack(m4, D < 4 ? D : 3, h);
+        } else {
+          reinterpret_cast<uint32_t*>(q + nb)[o] = ((uint32_t)e << 16) | (uint32_t)h;
+        }
         if (last) {
           if (!REWALK) {
 #pragma unroll
             for (int d = 0; d < K - 1; ++d) S.flags[mm[d]] = 3;
             S.flags[h] = 3;
           }
-          reinterpret_cast<uint16_t*>(q + nb + 4 * (int)nN)[o] = 0;
+          reinterpret_cast<uint16_t*>(q + nb + ES * (int)nN)[o] = 0;
         }
         ++o;
       }
@@ -742,7 +767,7 @@ struct BfsLevel {
     __syncthreads();
     lvl[D + 1] = nb;
     if constexpr (D + 1 < K) {
-      return BfsLevel<K, D + 1, NT>::template run<REWALK>(S, H, q, qbytes, out, nN, tid, pp);
+      return BfsLevel<K, D + 1, NT, WE>::template run<REWALK>(S, H, q, qbytes, out, nN, tid, pp);
     } else {
       out.C = nN;
       return out;
@@ -753,7 +778,7 @@ struct BfsLevel {
 // Cliques of the roots [r0, r1) (picker-0 positions).  Returns C = -1 when a level does not
 // fit the queue region; the caller then retries with fewer roots (root chunks, P4) and falls
 // back to the per-root DFS only when a single root does not fit.
-template <int K, bool REWALK, int NT>
+template <int K, bool REWALK, int NT, bool WE = false>
 __device__ __forceinline__ BfsOut<K> bfs_cliques(const FShared& S, FusedHdr& H, char* q,
                                                  int qbytes, int r0, int r1, bool get_cc,
                                                  uint32_t target, int tid,
@@ -781,8 +806,9 @@ __device__ __forceinline__ BfsOut<K> bfs_cliques(const FShared& S, FusedHdr& H, 
   __syncthreads();
   const int64_t n2 = ufl(block_scan_dpp32<NT>(cnt, nr, H.redi));   // (< n^2 < 2^31)
   constexpr bool last = K == 2;
-  if (K >= 4) out.fit = fminf(bfs_fit(n2, 65535), bfs_fit(n2 * (last ? 6 : 4), qbytes));
-  if (n2 > 65535 || n2 * (last ? 6 : 4) > qbytes) {
+  constexpr int ES = bfs_es<WE>();
+  if (K >= 4) out.fit = fminf(bfs_fit(n2, 65535), bfs_fit(n2 * (last ? ES + 2 : ES), qbytes));
+  if (n2 > 65535 || n2 * (last ? ES + 2 : ES) > qbytes) {
     out.fit = fminf(out.fit, 0.999f);
     return out;
   }
@@ -793,20 +819,21 @@ __device__ __forceinline__ BfsOut<K> bfs_cliques(const FShared& S, FusedHdr& H, 
     const int se = seg_end(r);
     for (int t = S.fwd[r]; t < se; ++t, ++o) {
       const int h = S.dst[t];
-      reinterpret_cast<uint32_t*>(q)[o] = ((uint32_t)r << 16) | (uint32_t)h;
+      if constexpr (WE) reinterpret_cast<uint2*>(q)[o] = make_uint2((uint32_t)r | ((uint32_t)h << 16), 0u);
+      else reinterpret_cast<uint32_t*>(q)[o] = ((uint32_t)r << 16) | (uint32_t)h;
       if (last) {
         if (!REWALK) {
           S.flags[r] = 3;
           S.flags[h] = 3;
         }
-        reinterpret_cast<uint16_t*>(q + 4 * (int)n2)[o] = 0;
+        reinterpret_cast<uint16_t*>(q + ES * (int)n2)[o] = 0;
       }
     }
   }
   __syncthreads();
   out.lvl[2] = 0;
   if constexpr (K > 2) {
-    return BfsLevel<K, 2, NT>::template run<REWALK>(S, H, q, qbytes, out, n2, tid, pp);
+    return BfsLevel<K, 2, NT, WE>::template run<REWALK>(S, H, q, qbytes, out, n2, tid, pp);
   } else {
     out.C = n2;
     return out;
@@ -1489,6 +1516,18 @@ void k_fused(FusedArgs A) {
   STAMP(4);   // scan
   STOP_AFTER(22);
   bool cc32 = false;   // the unions ran on u32 parents in cnt
+  // QG launches: the workgroup's HBM level-tree slot (claimed here when the edge sources do not
+  // fit dst's tail: they go to the slot, dead again by P4, which reuses it for the trees)
+  int qslot = -1;
+  uint16_t* esrc_g = nullptr;
+  if constexpr (QG) {
+    if (st2 == 0 && 2 * E > A.ecap && A.qg_base) {
+      if (tid == 0) H.qslot = qg_claim(A);
+      __syncthreads();
+      qslot = ufl(H.qslot);
+      if (qslot >= 0) esrc_g = reinterpret_cast<uint16_t*>(A.qg_base + (size_t)qslot * A.qg_bytes);
+    }
+  }
   if (st2 == 0) {
     // fill each list (already sorted: position order) and record each edge's source in dst's
     // unused tail when it has room; then union the edges one thread per edge (lock-free
@@ -1496,9 +1535,12 @@ void k_fused(FusedArgs A) {
 #ifdef RGC_X_BOXUNION   // experiment: union per box inside the fill
     const bool src_ok = false;
 #else
-    const bool src_ok = 2 * E <= A.ecap;
+    const bool src_ok = 2 * E <= A.ecap || (QG && esrc_g != nullptr);
 #endif
     uint16_t* esrc = S.dst + E;
+    // (QG: esrc_g in HBM when dst's tail is short; separate loops keep esrc's LDS accesses
+    // ds_* instructions instead of flat ones)
+    const bool src_hbm = QG && esrc_g != nullptr;
     auto fill_walk = [&](int i, int base, int cnt) {
       Stencil st;
       stencil_setup<K, W>(st, i, S, G);
@@ -1527,7 +1569,9 @@ void k_fused(FusedArgs A) {
           fill_walk(i, base, cnt);
         }
         S.flags[i] = 1;
-        if (src_ok) {
+        if (src_hbm) {
+          for (int e = 0; e < cnt; ++e) esrc_g[base + e] = (uint16_t)i;
+        } else if (src_ok) {
           for (int e = 0; e < cnt; ++e) esrc[base + e] = (uint16_t)i;
         } else {
           for (int e = 0; e < cnt; ++e) {
@@ -1541,7 +1585,27 @@ void k_fused(FusedArgs A) {
     __syncthreads();
     STAMP(5);   // fill
     STOP_AFTER(23);
-    if (src_ok) {
+    if (src_hbm) {
+      // sources from HBM (L2) in batches of 8 loads in flight per thread, then the unions
+      constexpr int UB = 8;
+      for (int e0 = tid; e0 < E; e0 += UB * FWG) {
+        uint32_t sv[UB];
+#pragma unroll
+        for (int u = 0; u < UB; ++u) {
+          const int e = e0 + u * FWG;
+          sv[u] = e < E ? esrc_g[e] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < UB; ++u) {
+          const int e = e0 + u * FWG;
+          if (e >= E) break;
+          const uint32_t h = S.dst[e];
+          S.flags[h] = 1;
+          uf_union32(S.cnt, sv[u], h);
+        }
+      }
+      __syncthreads();
+    } else if (src_ok) {
       for (int e = tid; e < E; e += FWG) {
         const uint32_t h = S.dst[e];
         S.flags[h] = 1;
@@ -1667,18 +1731,21 @@ void k_fused(FusedArgs A) {
   const int qbytes_lds = L.off_parent - qoff;
   char* q = smem + qoff;
   int qbytes = qbytes_lds;
-  int qslot = -1;
   if constexpr (QG) {
     // large micrographs: the level trees in an HBM slot (no root chunks to re-walk), the
-    // LDS region when no slot is free
-    if (tid == 0) H.qslot = A.qg_base ? qg_claim(A) : -1;
-    __syncthreads();
-    qslot = ufl(H.qslot);
+    // LDS region when no slot is free (P2 may have claimed the slot already for esrc)
+    if (qslot < 0) {
+      if (tid == 0) H.qslot = A.qg_base ? qg_claim(A) : -1;
+      __syncthreads();
+      qslot = ufl(H.qslot);
+    }
     if (qslot >= 0) {
       q = A.qg_base + (size_t)qslot * (size_t)A.qg_bytes;
       qbytes = A.qg_bytes;
     }
   }
+  // wide level-tree entries (members, not parent chains) in the HBM slot
+  const bool we = QG && K <= 4 && qslot >= 0;
   // Root chunks: all roots at once when the levels fit the queue region, else consecutive
   // root ranges (halved after a level overflows, doubled after a success).  Chunk i covers
   // roots [rs[i], rs[i+1]) and cliques [cs[i], cs[i+1]) of the micrograph's lexicographic
@@ -1710,8 +1777,12 @@ void k_fused(FusedArgs A) {
     if (tid == 0) { chtab[0] = 0; chtab[1] = 0; }
     while (ok && r0 < n0) {
       len = min(len, n0 - r0);
-      bo = bfs_cliques<K, false, NT>(S, H, q, qbytes, r0, r0 + len, get_cc, (uint32_t)target, tid,
-                                 c.pp);
+      if (QG && K <= 4 && qslot >= 0)
+        bo = bfs_cliques<K, false, NT, QG && K <= 4>(S, H, q, qbytes, r0, r0 + len, get_cc,
+                                                     (uint32_t)target, tid, c.pp);
+      else
+        bo = bfs_cliques<K, false, NT>(S, H, q, qbytes, r0, r0 + len, get_cc, (uint32_t)target,
+                                       tid, c.pp);
       if (bo.C < 0) {
         // shrink to the estimated fit of the overflowing level (demand grows about linearly
         // with the roots), with a small margin; strictly smaller each time
@@ -1735,7 +1806,7 @@ void k_fused(FusedArgs A) {
   } else if (bfs_ok) {
     // cliques = level-K tree entries (members by walking parents); their flag words follow
     c.cq_cap = (int)max(bo.C, (int64_t)1);
-    c.cq_ord = reinterpret_cast<uint16_t*>(q + bo.lvl[K] + 4 * (int)bo.C);
+    c.cq_ord = reinterpret_cast<uint16_t*>(q + bo.lvl[K] + (we ? 8 : 4) * (int)bo.C);
   } else {
     S.cbuf = reinterpret_cast<uint16_t*>(smem + qoff);   // (LDS even when QG)
     c.cq_cap = 0;   // the DFS only counts; P6 re-walks it chunk by chunk
@@ -1900,11 +1971,14 @@ void k_fused(FusedArgs A) {
         c1 = ufl((int)chtab[2 * ch + 3]);
         if constexpr (K >= 4) {
           if (ci > 0)
-            cur = bfs_cliques<K, true, NT>(S, H, q, qbytes, ufl((int)chtab[2 * ch]),
+            cur = we ? bfs_cliques<K, true, NT, QG && K <= 4>(S, H, q, qbytes, ufl((int)chtab[2 * ch]),
+                                       ufl((int)chtab[2 * ch + 2]), get_cc, (uint32_t)target,
+                                       tid, c.pp)
+                     : bfs_cliques<K, true, NT>(S, H, q, qbytes, ufl((int)chtab[2 * ch]),
                                        ufl((int)chtab[2 * ch + 2]), get_cc, (uint32_t)target,
                                        tid, c.pp);
         }
-        c.cq_ord = reinterpret_cast<uint16_t*>(q + cur.lvl[K] + 4 * (c1 - c0));
+        c.cq_ord = reinterpret_cast<uint16_t*>(q + cur.lvl[K] + (we ? 8 : 4) * (c1 - c0));
       } else {
         c0 = ci * cap;
         c1 = min(Cm, c0 + cap);
@@ -1934,7 +2008,8 @@ void k_fused(FusedArgs A) {
           return obase + (int64_t)(S.cnt[mem[0]] + ((rr.y >> 16) & 0x7FFF));
         }
         if (bfs_ok) {
-          BfsLevel<K, K, NT>::prefix(q, cur.lvl, (uint32_t)sl, mem);
+          if (we) BfsLevel<K, K, NT, QG && K <= 4>::prefix(q, cur.lvl, (uint32_t)sl, mem);
+          else BfsLevel<K, K, NT>::prefix(q, cur.lvl, (uint32_t)sl, mem);
         } else {
           const uint16_t* sb = S.cbuf + sl * K;
 #pragma unroll
