@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define RGC_ABI_VERSION 7
+#define RGC_ABI_VERSION 8
 
 /* flags for rgc_batch_in.flags */
 #define RGC_F_GET_CC         1u  /* --get_cc   (get_cliques.py:151-156) */
@@ -200,6 +200,10 @@ typedef struct rgc_ilp_in {
                             * column (0 elsewhere and for proven-optimal components), so a
                             * caller can certify a whole micrograph the way Gurobi's MIPGap
                             * does (sum of gaps <= 1e-4 x its objective) */
+  double time_limit_s;     /* ABI 8: seconds the branch-and-bound search of the 65..4096-clique
+                            * components may take (<= 0: no limit); components it does not
+                            * reach are packed and certified like the larger ones, components it
+                            * stops in keep their incumbent (status by the certified gap) */
 } rgc_ilp_in;
 int rgc_ilp_solve(rgc_ctx* ctx, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact);
 

@@ -72,7 +72,7 @@ enum DevBufId {
   D_IL_CPTR, D_IL_ROW, D_IL_W, D_IL_REP, D_IL_PAR, D_IL_ROOT, D_IL_CSIZE, D_IL_RCNT, D_IL_RCUR,
   D_IL_RPTR, D_IL_RCOLS, D_IL_CID, D_IL_CN, D_IL_COFF, D_IL_CCUR, D_IL_MEM, D_IL_LOC, D_IL_SCR,
   D_IL_BIG, D_IL_NBIG, D_IL_WSCR, D_IL_X, D_IL_EX, D_IL_RLOC, D_IL_CERT, D_IL_KEY, D_IL_ST,
-  D_IL_RMAX, D_IL_OWN, D_IL_LAM, D_IL_GRAD, D_IL_CS, D_IL_CNT, D_IL_GAP,
+  D_IL_RMAX, D_IL_OWN, D_IL_LAM, D_IL_GRAD, D_IL_CS, D_IL_CNT, D_IL_GAP, D_IL_STSAVE,
   D_COUNT
 };
 enum HostBufId {
@@ -1585,7 +1585,8 @@ int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) 
   TRY(ensure_dev(c, D_IL_OWN, nr * 4 + 4));
   TRY(ensure_dev(c, D_IL_LAM, nr * 8 + 8));
   TRY(ensure_dev(c, D_IL_GRAD, nr * 8 + 8));
-  TRY(ensure_dev(c, D_IL_CS, (ncomp + 1) * 8 * 8));
+  TRY(ensure_dev(c, D_IL_CS, (ncomp + 1) * 10 * 8));
+  TRY(ensure_dev(c, D_IL_STSAVE, nc));
   TRY(ensure_dev(c, D_IL_CNT, 16));
   A.cert = D<uint8_t>(c, D_IL_CERT);
   A.key = D<uint64_t>(c, D_IL_KEY);
@@ -1596,6 +1597,9 @@ int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) 
   A.grad = D<double>(c, D_IL_GRAD);
   A.cs = D<double>(c, D_IL_CS);
   A.count = D<unsigned int>(c, D_IL_CNT);
+  A.st_save = D<uint8_t>(c, D_IL_STSAVE);
+  // the wave search's time budget (ABI 8 rgc_ilp_in.time_limit_s; <= 0: none)
+  A.wave_budget = in->time_limit_s > 0.0 ? (uint64_t)(in->time_limit_s * 1e8) : 0;
   A.gap = nullptr;
   if (in->gap) {   // (ABI 6) per-component gaps: zero for proven components
     TRY(ensure_dev(c, D_IL_GAP, nc * 8));
@@ -1612,6 +1616,15 @@ int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) 
       HIPCHK(hipStreamSynchronize(s));
       if (*reinterpret_cast<uint32_t*>(H<int64_t>(c, H_TOTAL) + 3) == 0) break;
     }
+    return 0;
+  };
+  // Lagrangian repack of the flagged components (rgc_ilp.hip k_rp_*): greedy by reduced cost
+  // with the best multipliers, swaps, kept per component when better
+  auto repack = [&]() -> int {
+    rgc::launch_ilp_cert(s, 8, A);
+    TRY(rounds(1, 1 << 20));
+    TRY(rounds(2, 1 << 16));
+    rgc::launch_ilp_cert(s, 9, A);
     return 0;
   };
   if (n_big > 0) {
@@ -1640,6 +1653,8 @@ int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) 
     rgc::launch_ilp_cert(s, 3, A);
     for (int it = 0; it < 400; ++it) rgc::launch_ilp_cert(s, 4, A);
     rgc::launch_ilp_cert(s, 7, A);
+    // the packing repacked by reduced cost when better: it seeds the search's incumbent
+    TRY(repack());
     TRY(mark(c, "k_ilp_wave"));
     rgc::launch_ilp(s, 4, A, n_big, n_waves);
   }
@@ -1655,9 +1670,14 @@ int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) 
     TRY(rounds(2, 1 << 16));
     rgc::launch_ilp_cert(s, 3, A);
     // projected subgradient iterations of the Lagrangian bound (per component Polyak steps
-    // towards the primal; after 20 iterations without progress the step halves and lam
-    // restarts from the best one)
+    // towards the primal; after 40 iterations without progress the step shrinks and lam
+    // restarts from the best one), a repack by reduced cost from the multipliers, then more
+    // iterations with the better primal's steps
     for (int it = 0; it < 1000; ++it) rgc::launch_ilp_cert(s, 4, A);
+    TRY(repack());
+    for (int it = 0; it < 4000; ++it) rgc::launch_ilp_cert(s, 4, A);
+    TRY(repack());
+    for (int it = 0; it < 2000; ++it) rgc::launch_ilp_cert(s, 4, A);
     rgc::launch_ilp_cert(s, 5, A);
   }
   TRY(mark(c, "d2h_x"));

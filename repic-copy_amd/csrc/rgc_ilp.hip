@@ -26,6 +26,8 @@
 namespace rgc {
 
 constexpr int ILP_WG = 256;
+constexpr uint8_t ST_IN_SEED = 1;        // (= ST_IN below: the pre-search packing)
+constexpr uint8_t ILP_UNSEARCHED = 255;  // wave component skipped past the time budget
 constexpr int ILP_SMALL = 64;     // thread-per-component limit (one 64-bit mask)
 constexpr int ILP_BIG = 4096;     // wave-per-component limit (64 lanes x 64 bits)
 
@@ -298,12 +300,17 @@ __global__ __launch_bounds__(64) void k_ilp_wave(IlpArgs A, int n_big) {
   __shared__ int counter;
   const int lane = threadIdx.x;
   uint64_t* base = A.wscratch + (int64_t)blockIdx.x * A.wstride;
+  // (the launch's waves are all resident at once: each one's start is the launch's)
+  const uint64_t deadline =
+      A.wave_budget ? (uint64_t)__builtin_amdgcn_s_memrealtime() + A.wave_budget : 0;
   for (int bi = blockIdx.x; bi < n_big; bi += gridDim.x) {
     const int64_t comp = A.big[bi];
     const int n = A.comp_n[comp];
     int32_t* m = A.members + A.comp_off[comp];
-    if (n > ILP_BIG) {
-      for (int i = lane; i < n; i += 64) { A.x[m[i]] = 0; A.exact[m[i]] = 0; }
+    // past the launch's time budget: not searched (the certification packs it: ST_UNSEARCHED)
+    const bool late = deadline && (uint64_t)__builtin_amdgcn_s_memrealtime() > deadline;
+    if (n > ILP_BIG || late) {
+      for (int i = lane; i < n; i += 64) { A.x[m[i]] = 0; A.exact[m[i]] = late ? ILP_UNSEARCHED : 0; }
       continue;
     }
     const int W = (n + 63) / 64;
@@ -450,6 +457,29 @@ __global__ __launch_bounds__(64) void k_ilp_wave(IlpArgs A, int n_big) {
     // relative; run_ilp.py:50-63 solves with default parameters) of it - status GAP_OK
     const double root_bound = lag ? fmin(bound(P), lag_bound(P)) : bound(P);
     double best = -1.0, cur = 0.0;
+    // incumbent seeded with the pre-search packing (greedy + swaps, A.st of the cert-3
+    // components): the search prunes against it from the first node and may stop at once
+    if (lag && A.st) {
+      uint64_t bs = 0;
+      double v = 0.0;
+      if (lane < W)
+        for (int b = 0; b < 64; ++b) {
+          const int i = lane * 64 + b;
+          if (i >= n) break;
+          if (A.st[m[i]] == ST_IN_SEED) {
+            bs |= 1ull << b;
+            v += wl[i];
+          }
+        }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      // (a hair below its value: a packing of equal weight met in the search's heaviest-first
+      // order still replaces it, so ties resolve as without the seed)
+      if (v > 0.0) {
+        best = v * (1.0 - 1e-12);
+        best_set = bs;
+      }
+    }
     int depth = 0;
     int64_t nodes = 0;
     uint8_t status = RGC_ILP_OPTIMAL;
@@ -457,9 +487,15 @@ __global__ __launch_bounds__(64) void k_ilp_wave(IlpArgs A, int n_big) {
     // components above 1024 cliques get node_limit * 16 / W nodes (a whole C5 micrograph's
     // medium components ran 27 s at 2^22 nodes each)
     const int64_t node_cap = A.node_limit * 16 / (W > 16 ? W : 16);
-    for (;;) {
+    for (; status == RGC_ILP_OPTIMAL;) {
       bool back = false;
       if (++nodes > node_cap) { status = RGC_ILP_NODE_LIMIT; break; }
+      // the launch's time budget, checked every 1024 nodes
+      if (deadline && (nodes & 1023) == 0 &&
+          (uint64_t)__builtin_amdgcn_s_memrealtime() > deadline) {
+        status = RGC_ILP_NODE_LIMIT;
+        break;
+      }
       const uint64_t nz = __ballot(P != 0);
       if (nz == 0) {
         if (cur > best) {
@@ -547,7 +583,8 @@ __global__ __launch_bounds__(64) void k_ilp_wave(IlpArgs A, int n_big) {
 //   * RGC_ILP_GAP_OK when lbest - primal <= 1e-4 primal, else the packing with status
 //     NODE_LIMIT / HEURISTIC.
 constexpr uint8_t ST_UND = 0, ST_IN = 1, ST_OUT = 2, ST_NONE = 3;
-constexpr int CS = 8;   // doubles per component record: lsum g2 lbest mu primal step stall flag
+constexpr int CS = 10;  // doubles per component record: lsum g2 lbest mu primal step stall flag
+                        // repacked-primal (spare)
 
 __device__ __forceinline__ int64_t ilp_comp(const IlpArgs& A, int64_t c) {
   return A.comp_id[A.parent[c]];
@@ -562,13 +599,14 @@ __global__ __launch_bounds__(ILP_WG) void k_cert_flag(IlpArgs A) {
   if (comp >= A.n_comp) return;
   const int n = A.comp_n[comp];
   uint8_t f = 0;
-  if (n > ILP_BIG) f = 2;
-  else if (n > 1 && A.exact[A.members[A.comp_off[comp]]] == 0) f = 1;
+  const uint8_t ex = n > 1 ? A.exact[A.members[A.comp_off[comp]]] : 1;
+  if (n > ILP_BIG || ex == ILP_UNSEARCHED) f = 2;
+  else if (ex == 0) f = 1;
   A.cert[comp] = f;
   if (f) atomicAdd(A.count + 1, 1u);   // flagged components (the host skips the rest when 0)
   double* cs = A.cs + comp * CS;
   cs[0] = 0.0; cs[1] = 0.0; cs[2] = INFINITY; cs[3] = 2.0; cs[4] = 0.0; cs[5] = 0.0; cs[6] = 0.0;
-  cs[7] = 0.0;
+  cs[7] = 0.0; cs[8] = 0.0; cs[9] = 0.0;
 }
 
 // before the wave search: components of 65..ILP_BIG cliques get multipliers for the search's
@@ -582,7 +620,7 @@ __global__ __launch_bounds__(ILP_WG) void k_cert_flag_pre(IlpArgs A) {
   if (f) atomicAdd(A.count + 1, 1u);
   double* cs = A.cs + comp * CS;
   cs[0] = 0.0; cs[1] = 0.0; cs[2] = INFINITY; cs[3] = 2.0; cs[4] = 0.0; cs[5] = 0.0; cs[6] = 0.0;
-  cs[7] = 0.0;
+  cs[7] = 0.0; cs[8] = 0.0; cs[9] = 0.0;
 }
 // after the pre-search subgradient: the best multipliers (kept in rmax) become lam
 __global__ __launch_bounds__(ILP_WG) void k_lr_take_best(IlpArgs A) {
@@ -759,8 +797,8 @@ __global__ __launch_bounds__(ILP_WG) void k_lr_step(IlpArgs A) {
   } else {
     cs[6] += 1.0;
   }
-  if (cs[6] >= 20.0) {          // no progress: halve the step, restart from the best lam
-    cs[3] *= 0.5;
+  if (cs[6] >= 40.0) {          // no progress: shrink the step, restart from the best lam
+    cs[3] *= 0.7;
     cs[6] = 0.0;
     cs[7] = 2.0;
   }
@@ -781,6 +819,69 @@ __global__ __launch_bounds__(ILP_WG) void k_lr_lam(IlpArgs A) {
   else A.lam[r] = fmax(0.0, A.lam[r] - cs[5] * A.grad[r]);
   A.grad[r] = 0.0;
 }
+// Lagrangian repack (certification): the LP of these models is nearly integral (a full C5
+// micrograph: 229 fractional of 705,588 columns), and with multipliers near the LP duals the
+// columns of positive reduced cost w_c - sum_r lam_r are nearly its support.  So the packing
+// is rebuilt greedily by reduced cost (heaviest reduced cost first), improved by the same
+// swaps, and kept per component when it beats the weight-greedy one.
+__device__ __forceinline__ uint32_t sortable_f32(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+// rows of flagged components: lam = the best multipliers (rmax), claims and owners cleared
+__global__ __launch_bounds__(ILP_WG) void k_rp_rows(IlpArgs A) {
+  const int64_t r = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (r >= A.n_rows) return;
+  const int64_t comp = ilp_row_comp(A, r);
+  if (comp < 0 || A.cert[comp] == 0) return;
+  A.lam[r] = reinterpret_cast<const double*>(A.rmax)[r];
+  A.rmax[r] = 0;
+  A.owner[r] = -1;
+}
+// columns: save the packing, key by reduced cost, undecided again
+__global__ __launch_bounds__(ILP_WG) void k_rp_cols(IlpArgs A) {
+  const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (c >= A.n_cols || A.st[c] == ST_NONE) return;
+  if (A.cert[ilp_comp(A, c)] == 0) return;
+  A.st_save[c] = A.st[c];
+  const double w = A.w[c];
+  double rc = w;
+  for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e) rc -= A.lam[A.row_idx[e]];
+  A.key[c] = ((uint64_t)sortable_f32((float)rc) << 32) | (uint32_t)~(uint32_t)c;
+  A.st[c] = w > 0.0 ? ST_UND : ST_OUT;
+}
+__global__ __launch_bounds__(ILP_WG) void k_rp_primal(IlpArgs A) {
+  const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (c >= A.n_cols || A.st[c] != ST_IN) return;
+  const int64_t comp = ilp_comp(A, c);
+  if (A.cert[comp] != 0) atomicAdd(A.cs + comp * CS + 8, A.w[c]);
+}
+// keep the better packing per component (ties: the earlier one)
+__global__ __launch_bounds__(ILP_WG) void k_rp_pick(IlpArgs A) {
+  const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (c >= A.n_cols || A.st[c] == ST_NONE) return;
+  const int64_t comp = ilp_comp(A, c);
+  if (A.cert[comp] == 0) return;
+  const double* cs = A.cs + comp * CS;
+  if (!(cs[8] > cs[4])) A.st[c] = A.st_save[c];
+}
+__global__ __launch_bounds__(ILP_WG) void k_rp_comps(IlpArgs A) {
+  const int64_t comp = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (comp >= A.n_comp || A.cert[comp] == 0) return;
+  double* cs = A.cs + comp * CS;
+  cs[4] = fmax(cs[4], cs[8]);
+  cs[8] = 0.0;
+}
+// rows: the best multipliers back where the subgradient's restarts read them
+__global__ __launch_bounds__(ILP_WG) void k_rp_best(IlpArgs A) {
+  const int64_t r = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (r >= A.n_rows) return;
+  const int64_t comp = ilp_row_comp(A, r);
+  if (comp < 0 || A.cert[comp] == 0) return;
+  reinterpret_cast<double*>(A.rmax)[r] = A.lam[r];
+  A.owner[r] = -1;
+}
+
 // x and the component statuses
 __global__ __launch_bounds__(ILP_WG) void k_cert_final(IlpArgs A) {
   const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
@@ -844,6 +945,16 @@ void launch_ilp_cert(hipStream_t stream, int phase, const IlpArgs& A) {
       break;
     case 7:
       if (nbr) RGC_L(k_lr_take_best, nbr);
+      break;
+    case 8:   // Lagrangian repack: setup (then greedy rounds, swap rounds, phase 9)
+      if (nbr) RGC_L(k_rp_rows, nbr);
+      RGC_L(k_rp_cols, nbc);
+      break;
+    case 9:   // repack: value, pick per component, multipliers restored
+      RGC_L(k_rp_primal, nbc);
+      RGC_L(k_rp_pick, nbc);
+      RGC_L(k_rp_comps, nbk);
+      if (nbr) RGC_L(k_rp_best, nbr);
       break;
   }
 #undef RGC_L

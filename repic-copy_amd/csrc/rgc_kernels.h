@@ -294,9 +294,14 @@ struct IlpArgs {
   int32_t* owner;             // [n_rows] chosen column covering the row, -1
   double* lam;                // [n_rows] Lagrange multipliers
   double* grad;               // [n_rows] subgradient (cover count in between)
-  double* cs;                 // [n_comp * 8] per component: lsum g2 lbest mu primal step stall
+  double* cs;                 // [n_comp * CS] per component: lsum g2 lbest mu primal step stall
+                              // flag, repacked primal
   unsigned int* count;        // round counter
   double* gap;                // optional [n_cols]: component bound - packing at its first column
+  uint8_t* st_save;           // [n_cols] certification: the packing before a Lagrangian repack
+  uint64_t wave_budget;       // wave search: s_memrealtime ticks (100 MHz) after its start past
+                              // which no new component is searched and running searches stop
+                              // (0: none)
 };
 int ilp_small_max();
 int ilp_big_max();

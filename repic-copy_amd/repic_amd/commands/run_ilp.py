@@ -52,6 +52,9 @@ def add_arguments(parser):
                         help="filter for the number of expected particles (int)")
     parser.add_argument("--node_limit", type=int, default=0,
                         help="branch-and-bound nodes per conflict component (0: 2^22)")
+    parser.add_argument("--time_limit", type=float, default=ilp.DEFAULT_TIME_LIMIT_S,
+                        help="seconds the branch and bound may search (<= 0: no limit; "
+                             "unfinished components are certified by their Lagrangian bound)")
     parser.add_argument("--device", type=int, default=None,
                         help="HIP device (default: $LOCAL_RANK or 0)")
 
@@ -85,7 +88,9 @@ def main(args):
         ctx = _lib.Context(dev)
         try:
             xs, status, rgap = solve_batch(ctx, mats, weights, getattr(args, "node_limit", 0),
-                                           statuses=True, gaps=True)
+                                           statuses=True, gaps=True,
+                                           time_limit=getattr(args, "time_limit",
+                                                              ilp.DEFAULT_TIME_LIMIT_S))
         finally:
             ctx.close()
     share = (time.time() - t0) / max(1, len(mats))

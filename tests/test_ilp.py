@@ -135,7 +135,8 @@ def _check(problems, xs, status, inexact_gap=None):
         assert abs(obj - objr) <= 1e-12 * max(1.0, objr), (obj, objr)
         if np.array_equal(x, xr):
             uniq += 1
-    print("inexact micrographs:", len(gaps), "relative gaps:", gaps)
+    print("inexact micrographs:", len(gaps), "relative gaps:", gaps, "GAP_OK:",
+          sum(1 for s_ in status if s_ == GAP_OK))
     return uniq
 
 
@@ -147,7 +148,11 @@ def test_gpu_ilp_matches_exact_solvers_on_golden():
     ctx = _lib.Context(0)
     xs, st = solve_batch(ctx, [a for a, _ in probs], [w for _, w in probs], statuses=True)
     ctx.close()
-    assert _check(probs, xs, st) >= len(probs) - 2
+    # micrographs proven OPTIMAL: the packing is HiGHS' one where the optimum is unique (all
+    # but ties); GAP_OK ones (a search stopped within Gurobi's MIPGap) are checked by _check
+    from repic_amd.ilp import OPTIMAL
+    n_opt = sum(1 for s_ in st if s_ == OPTIMAL)
+    assert _check(probs, xs, st) >= n_opt - 2 and n_opt >= len(probs) - 4
 
 
 @pytest.mark.gpu
@@ -331,8 +336,9 @@ def test_gpu_ilp_c3_default_limit_certified_per_micrograph():
         gap = (objr - obj) / objr
         print("C3 default limit: status", s, "certified gap", g, "gap vs HiGHS", gap)
         assert -1e-12 <= gap <= g + 1e-12 and gap <= 5e-3
-        if s in (OPTIMAL, GAP_OK):
-            assert g <= 1e-4
+        # round 5 (seeded search, Lagrangian repack): every crowded C3 micrograph certified
+        # within Gurobi's MIPGap at the default limits
+        assert s in (OPTIMAL, GAP_OK) and g <= 1e-4
 
 
 @pytest.mark.gpu
@@ -372,6 +378,9 @@ def test_gpu_ilp_full_c5_micrograph():
     print(f"full C5 micrograph: {C} cliques, {V} boxes, status {st[0]}, objective {obj:.6f}, "
           f"certified relative gap {rgap[0]:.3e}, solve {dt:.2f} s")
     assert st[0] in (OPTIMAL, GAP_OK, HEURISTIC)
+    # round 5: a certified gap within 1e-3 inside the default 5 s search budget (the LP bound
+    # of this micrograph, scipy/HiGHS on the CPU, is 1115.688: within 6e-4 of the packing)
+    assert rgap[0] <= 1e-3 and dt <= 10.0, (rgap[0], dt)
     assert 0.0 <= rgap[0] < 0.05
 
 
@@ -402,7 +411,7 @@ def test_run_ilp_runtime_line_is_reference_format(tmp_path, monkeypatch):
         def close(self):
             pass
 
-    def _solve(ctx, mats, weights, node_limit=0, statuses=False, gaps=False):
+    def _solve(ctx, mats, weights, node_limit=0, statuses=False, gaps=False, time_limit=None):
         return [np.array([1, 0], np.uint8)], [ilp.GAP_OK], [2.5e-5]
 
     monkeypatch.setattr(run_ilp._lib, "Context", _Ctx)
