@@ -390,10 +390,11 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   }
   st_p0[n_mg] = (int32_t)n_roots;
 
-  TRY(ensure_dev(c, D_BOXOFF, nbo * 4));
-  TRY(ensure_dev(c, D_CELLOFF, (n_mg + 1) * 4));
-  TRY(ensure_dev(c, D_P0OFF, (n_mg + 1) * 4));
-  TRY(ensure_dev(c, D_IDBASE, n_mg * 8));
+  // the per-micrograph metadata (box offsets, cell offsets, picker-0 prefix, id bases) go up
+  // in ONE copy of the host staging block; the device block has the same layout
+  const size_t meta_bytes = (size_t)(reinterpret_cast<char*>(st_id + n_mg) -
+                                     reinterpret_cast<char*>(st_bo));
+  TRY(ensure_dev(c, D_BOXOFF, meta_bytes));
   TRY(ensure_dev(c, D_GRID, n_mg * sizeof(MgGrid)));
   TRY(ensure_dev(c, D_CELLSTART, cells * 4));
   TRY(ensure_dev(c, D_SX, N * 8));
@@ -431,29 +432,37 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
 
   hipStream_t s = c->stream;
   TRY(mark(c, "h2d_meta"));
-  HIPCHK(hipMemcpyAsync(D<void>(c, D_BOXOFF), st_bo, nbo * 4, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(D<void>(c, D_CELLOFF), st_co, (n_mg + 1) * 4, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(D<void>(c, D_P0OFF), st_p0, (n_mg + 1) * 4, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(D<void>(c, D_IDBASE), st_id, n_mg * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(D<void>(c, D_BOXOFF), st_bo, meta_bytes, hipMemcpyHostToDevice, s));
+  const int32_t* d_co = D<int32_t>(c, D_BOXOFF) + (st_co - st_bo);
+  const int32_t* d_p0 = D<int32_t>(c, D_BOXOFF) + (st_p0 - st_bo);
+  const int64_t* d_id = reinterpret_cast<const int64_t*>(
+      D<char>(c, D_BOXOFF) + (reinterpret_cast<char*>(st_id) - reinterpret_cast<char*>(st_bo)));
   TRY(mark(c, "memset"));
-  HIPCHK(hipMemsetAsync(D<void>(c, D_HASEDGE), 0, N, s));
-  HIPCHK(hipMemsetAsync(D<void>(c, D_CSIZE), 0, N * 4, s));
-  HIPCHK(hipMemsetAsync(D<void>(c, D_INCL), 0, N, s));
-  HIPCHK(hipMemsetAsync(D<void>(c, D_CCOUNT), 0, N * 4, s));
-  HIPCHK(hipMemsetAsync(D<void>(c, D_VLIST), 0, N * 4, s));   // row-rank bucket counters
-  HIPCHK(hipMemsetAsync(D<void>(c, D_RFLAG), 0, N, s));
-  HIPCHK(hipMemsetAsync(D<void>(c, D_DFSMG), 0, n_mg, s));
-  HIPCHK(hipMemsetAsync(D<void>(c, D_INSKEY), 0xff, N * 8, s));
-  if (get_cc) HIPCHK(hipMemsetAsync(D<void>(c, D_COMPMIN), 0xff, N * 8, s));
+  // the level loop's first count array (non-roots stay 0) is zeroed with the others
+  TRY(ensure_dev(c, D_LCNT, N * 4));
+  {
+    rgc::FillSegs F{};
+    F.add(D<void>(c, D_HASEDGE), N, 0);
+    F.add(D<void>(c, D_CSIZE), N * 4, 0);
+    F.add(D<void>(c, D_INCL), N, 0);
+    F.add(D<void>(c, D_CCOUNT), N * 4, 0);
+    F.add(D<void>(c, D_VLIST), N * 4, 0);   // row-rank bucket counters
+    F.add(D<void>(c, D_RFLAG), N, 0);
+    F.add(D<void>(c, D_DFSMG), n_mg, 0);
+    F.add(D<void>(c, D_INSKEY), N * 8, 0xff);
+    F.add(D<void>(c, D_LCNT), N * 4, 0);
+    if (get_cc) F.add(D<void>(c, D_COMPMIN), N * 8, 0xff);
+    rgc::launch_fill_multi(s, F);
+  }
 
   const int32_t* bo = D<int32_t>(c, D_BOXOFF);
   TRY(mark(c, "k1_bin"));
-  launch_bin(s, n_mg, k, B, bo, D<int32_t>(c, D_CELLOFF), x, y, D<MgGrid>(c, D_GRID),
+  launch_bin(s, n_mg, k, B, bo, d_co, x, y, D<MgGrid>(c, D_GRID),
              D<int32_t>(c, D_CELLSTART), D<double>(c, D_SX), D<double>(c, D_SY),
              D<int32_t>(c, D_SBOX), D<uint8_t>(c, D_SPICK), D<int32_t>(c, D_SMG),
              D<int32_t>(c, D_BMG), D<uint8_t>(c, D_BPICK), bin_wide, max_n);
   TRY(mark(c, "k2_pairs_count"));
-  launch_pairs(s, false, (int)N, k, B, two_b2, bo, D<int32_t>(c, D_CELLOFF), D<MgGrid>(c, D_GRID),
+  launch_pairs(s, false, (int)N, k, B, two_b2, bo, d_co, D<MgGrid>(c, D_GRID),
                D<int32_t>(c, D_CELLSTART), D<double>(c, D_SX), D<double>(c, D_SY),
                D<int32_t>(c, D_SBOX), D<uint8_t>(c, D_SPICK), D<int32_t>(c, D_SMG),
                D<int32_t>(c, D_FWDCNT), nullptr, nullptr, nullptr);
@@ -470,7 +479,7 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   TRY(ensure_dev(c, D_ADJG, E * 8));
   if (want_ji) TRY(ensure_dev(c, D_EJI, E * 8));   // (the edge JIs feed the RGC_F_EDGES dump only)
   TRY(mark(c, "k2_pairs_fill"));
-  launch_pairs(s, true, (int)N, k, B, two_b2, bo, D<int32_t>(c, D_CELLOFF), D<MgGrid>(c, D_GRID),
+  launch_pairs(s, true, (int)N, k, B, two_b2, bo, d_co, D<MgGrid>(c, D_GRID),
                D<int32_t>(c, D_CELLSTART), D<double>(c, D_SX), D<double>(c, D_SY),
                D<int32_t>(c, D_SBOX), D<uint8_t>(c, D_SPICK), D<int32_t>(c, D_SMG),
                D<int32_t>(c, D_FWDCNT), D<int64_t>(c, D_FWDOFF), D<int32_t>(c, D_EDST),
@@ -490,7 +499,7 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   CliqueArgs A;
   A.k = k; A.flags = get_cc | (multi << 1); A.n_mg = n_mg; A.n_roots = n_roots; A.C = 0;
   A.B = B; A.two_b2 = two_b2;
-  A.box_off = bo; A.p0off = D<int32_t>(c, D_P0OFF); A.id_base = D<int64_t>(c, D_IDBASE);
+  A.box_off = bo; A.p0off = d_p0; A.id_base = d_id;
   A.x = x; A.y = y; A.score = sc; A.bmg = D<int32_t>(c, D_BMG); A.bpick = D<uint8_t>(c, D_BPICK);
   A.fwd_off = D<int64_t>(c, D_FWDOFF); A.e_dst = D<int32_t>(c, D_EDST);
   A.parent = D<int32_t>(c, D_PARENT); A.st = D<MgStat>(c, D_STAT);
@@ -527,7 +536,7 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
     L.cnt = D<int32_t>(c, D_LCNT);
     L.off = D<int64_t>(c, D_LOFF);
     TRY(mark(c, leaf ? "k5_leaf_count" : "k5_level_count"));
-    if (first) HIPCHK(hipMemsetAsync(L.cnt, 0, N * 4, s));   // non-roots stay 0
+    // (first level: L.cnt was zeroed with the per-box arrays; non-roots stay 0)
     if (launch_clique_level(s, first, leaf, false, A, L) != 0) return fail("unsupported k");
     launch_scan(s, L.n_items, L.cnt, D<int64_t>(c, D_LOFF), D<int64_t>(c, D_TILES), d_tot + 2);
     HIPCHK(hipMemcpyAsync(h_tot + 1, d_tot + 1, 16, hipMemcpyDeviceToHost, s));

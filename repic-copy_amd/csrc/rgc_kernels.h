@@ -207,6 +207,17 @@ void launch_pairs(hipStream_t stream, bool fill, int N, int k, double B, double 
                   const int32_t* cell_start, const double* sx, const double* sy,
                   const int32_t* sbox, const uint8_t* spick, const int32_t* smg,
                   int32_t* fwd_cnt, const int64_t* fwd_off, int32_t* e_dst, double* e_ji);
+// up to 16 memsets in one launch (k_fill_multi): pointers 16-byte aligned
+struct FillSegs {
+  int n;
+  void* p[16];
+  size_t bytes[16];
+  uint32_t val[16];
+  void add(void* ptr, size_t b, uint32_t v) {
+    if (n < 16 && b > 0) { p[n] = ptr; bytes[n] = b; val[n] = v & 0xFF; ++n; }
+  }
+};
+void launch_fill_multi(hipStream_t stream, const FillSegs& F);
 int64_t scan_tiles_needed(int64_t n);
 void launch_scan(hipStream_t stream, int64_t n, const int32_t* in, int64_t* out,
                  int64_t* tile_buf, int64_t* total);
