@@ -583,11 +583,17 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   launch_clique_level(s, k == 2, true, true, A, L);
   TRY(mark(c, "k5_dfs_fill"));
   launch_cliques_dfs(s, true, (int)N, A);
-  TRY(ensure_dev(c, D_EXLIST, (C + (C + 63) / 64) * 8));
+  // exact list [C], ballot words [ceil(C / 64)], per compaction wave: offsets and counts
+  const int64_t exw = (C + 63) / 64, exnw = (exw + 63) / 64;
+  TRY(ensure_dev(c, D_EXLIST, (C + exw + exnw + 1) * 8 + exnw * 4 + 16));
+  TRY(ensure_dev(c, D_TILES, scan_tiles_needed(exnw + 1) * 8));
   A.exlist = D<int64_t>(c, D_EXLIST);
   A.exmask = reinterpret_cast<uint64_t*>(A.exlist + C);
-  A.excount = reinterpret_cast<unsigned long long*>(d_tot + 3);   // rank scan total is dead
-  HIPCHK(hipMemsetAsync(A.excount, 0, 8, s));
+  A.exwoff = reinterpret_cast<int64_t*>(A.exmask + exw);
+  A.exwtot = reinterpret_cast<int32_t*>(A.exwoff + exnw + 1);
+  A.tiles = D<int64_t>(c, D_TILES);
+  // the exact list's length: the compaction scan's total (the rank scan's total is dead)
+  A.excount = reinterpret_cast<unsigned long long*>(d_tot + 3);
   TRY(ensure_dev(c, D_PK, (size_t)N * 16));
   A.pk = D<double>(c, D_PK);
   TRY(mark(c, "k5_pack"));

@@ -661,23 +661,33 @@ __global__ __launch_bounds__(WG) RGC_EPI_WPE void k5_epilogue(CliqueArgs A) {
 // The deferred cliques as a list: one wave per 64 ballot words (4096 cliques) ranks their set
 // bits with a DPP scan of the word popcounts and reserves its slice of the list with one
 // atomic (C / 4096 atomics per launch instead of one per epilogue wave).
-__global__ __launch_bounds__(WG) void k5_ex_compact(CliqueArgs A) {
+// The exact list without a shared counter: per compaction wave (64 ballot words = 4096
+// cliques) its count (k5_ex_wtot), a one-pass scan of the counts, then each wave writes its
+// slice (k5_ex_write).  (k5_ex_compact's one atomic per wave on one word: 15k serialised
+// returning atomics per C5 step, ~0.16 ms, replaced in round 5.)
+__global__ __launch_bounds__(WG) void k5_ex_wtot(CliqueArgs A) {
   const int lane = threadIdx.x & 63;
   const int64_t nwords = (A.C + 63) >> 6;
-  const int64_t w0 = (((int64_t)blockIdx.x * WG + threadIdx.x) >> 6) * 64;
+  const int64_t wv = ((int64_t)blockIdx.x * WG + threadIdx.x) >> 6;
+  const int64_t w0 = wv * 64;
+  if (w0 >= nwords) return;   // wave-uniform
+  const uint64_t word = w0 + lane < nwords ? A.exmask[w0 + lane] : 0ull;
+  const int total = __shfl(wave_incl_add32(__popcll(word)), 63);
+  if (lane == 0) A.exwtot[wv] = total;
+}
+__global__ __launch_bounds__(WG) void k5_ex_write(CliqueArgs A) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwords = (A.C + 63) >> 6;
+  const int64_t wv = ((int64_t)blockIdx.x * WG + threadIdx.x) >> 6;
+  const int64_t w0 = wv * 64;
   if (w0 >= nwords) return;   // wave-uniform
   const uint64_t word = w0 + lane < nwords ? A.exmask[w0 + lane] : 0ull;
   const int cnt = __popcll(word);
   const int incl = wave_incl_add32(cnt);
-  const int total = __shfl(incl, 63);
-  if (total == 0) return;
-  unsigned long long base = 0;
-  if (lane == 0) base = atomicAdd(A.excount, (unsigned long long)total);
-  base = ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(base >> 32), 0) << 32) |
-         (uint32_t)__shfl((int)(uint32_t)base, 0);
-  int64_t o = (int64_t)base + incl - cnt;
+  int64_t o = A.exwoff[wv] + incl - cnt;
   for (uint64_t w = word; w; w &= w - 1) A.exlist[o++] = ((w0 + lane) << 6) + __builtin_ctzll(w);
 }
+
 
 // Consensus (and --multi_out node order) of the cliques k5_epilogue deferred: exact f64
 // weighted degrees (get_cliques.py:182-183) and, on ties, the first tied member in networkx's
@@ -783,6 +793,13 @@ void launch_clique_setup(hipStream_t stream, int N, const CliqueArgs& A) {
 #ifndef RGC_EXGRID
 #define RGC_EXGRID 1024
 #endif
+static void ex_compact(hipStream_t stream, const CliqueArgs& A, int64_t nb) {
+  const int64_t nwv = (((A.C + 63) >> 6) + 63) / 64;   // compaction waves
+  hipLaunchKernelGGL(k5_ex_wtot, dim3((nb + 63) / 64), dim3(WG), 0, stream, A);
+  launch_scan(stream, nwv, A.exwtot, A.exwoff, A.tiles, reinterpret_cast<int64_t*>(A.excount));
+  hipLaunchKernelGGL(k5_ex_write, dim3((nb + 63) / 64), dim3(WG), 0, stream, A);
+}
+
 int launch_clique_epilogue(hipStream_t stream, bool exact_pass, const CliqueArgs& A) {
   const int64_t nb = (A.C + WG - 1) / WG;
   if (nb <= 0) return 0;
@@ -792,7 +809,7 @@ int launch_clique_epilogue(hipStream_t stream, bool exact_pass, const CliqueArgs
     if (!exact_pass)                                                                     \
       hipLaunchKernelGGL((k5_epilogue<KK>), dim3((nb + 1) / 2), dim3(WG), 0, stream, A); \
     else {                                                                               \
-      hipLaunchKernelGGL(k5_ex_compact, dim3((nb + 63) / 64), dim3(WG), 0, stream, A);   \
+      ex_compact(stream, A, nb);                                                         \
       hipLaunchKernelGGL((k5_epi_exact<KK>), dim3(std::min<int64_t>(nb, RGC_EXGRID)),      \
                          dim3(WG), 0, stream, A);                                        \
     }                                                                                    \

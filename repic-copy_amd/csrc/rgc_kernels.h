@@ -188,6 +188,9 @@ struct CliqueArgs {
                              // ballot word per epilogue wave) ...
   int64_t* exlist;           // [C] ... and as a list (k5_ex_compact)
   unsigned long long* excount;
+  int32_t* exwtot;            // [ceil(C / 4096)] deferred cliques per compaction wave
+  int64_t* exwoff;            // [ceil(C / 4096) + 1] their scanned offsets
+  int64_t* tiles;             // scan tile buffer (launch_scan)
   int64_t dfs_base;          // first output clique of the DFS route
   int32_t* members;
   int32_t* rows;
