@@ -10,8 +10,10 @@ ranks (weak scaling, no collective in the hot path).
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5] [--n_mg M]
 
 Prints ONE JSON line on rank 0 (driver contract), with "roofline" (dominant kernel, HIP
-events over the timed region) and "cpu_baseline" (the oracle's faithful per-pair loop on
-a bounded sample, 1 core).
+events around each launch) and "cpu_baseline" (the oracle's faithful per-pair loop on a
+bounded sample, 1 core).  Steps are pipelined on two contexts, by default on two streams so
+that step i+1's workgroups run in step i's drain tail (--streams 1 serialises them); the
+roofline's per-launch durations then come from serialised steps timed after the timed region.
 """
 from __future__ import annotations
 
@@ -301,6 +303,7 @@ def derived_bound(rec, kernel, alg_bytes, kernel_ms, dv_kernel="k_fused"):
 
 
 TIME_EVERY = 4   # pipelined steps: one in TIME_EVERY carries the HIP timing events
+SER_STEPS = 8    # two-stream runs: serialised steps timed with HIP events for the roofline
 
 
 class Env:
@@ -330,7 +333,7 @@ class Env:
 
 
 def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=False,
-            lazy_stats=True):
+            lazy_stats=True, streams=1):
     """Time ``steps`` steps of the hot path over one synthetic batch of ``config`` (n_mg
     micrographs per rank, inputs resident in HBM): barrier + synchronize on both sides, max
     over ranks.  Returns (report dict, cfg, this rank's micrographs)."""
@@ -377,9 +380,14 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
     # pipelined steps (default): two contexts on that one stream, rgc_submit / rgc_wait, so the
     # host side of step i+1 (planning, launch) overlaps the device work of step i while the
     # kernels stay serialised; every step runs the whole hot path into its own context's
-    # outputs and is waited for
+    # outputs and is waited for.  streams=2: the second context on a stream of its own, so
+    # step i+1's workgroups fill the CUs step i's drain tail leaves idle
     pipeline = not (host_io or no_pipeline)
-    ctxs = [ctx, _lib.Context(env.local, stream)] if pipeline else [ctx]
+    if pipeline and streams == 2:
+        tstream2 = torch.cuda.Stream(dev)
+        ctxs = [ctx, _lib.Context(env.local, tstream2.cuda_stream)]
+    else:
+        ctxs = [ctx, _lib.Context(env.local, stream)] if pipeline else [ctx]
 
     def step(timing=False):
         if host_io:
@@ -431,6 +439,7 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
                     ktimes[name] = ktimes.get(name, 0.0) + ms
         return r
 
+    overlap = pipeline and streams == 2
     try:
         if warmup:
             steps_run(warmup, False)
@@ -439,13 +448,25 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         ktimes = {}
-        r = steps_run(steps, True, ktimes)
+        # overlapping steps: no timing events in the timed region (a launch's events would span
+        # the other stream's workgroups too); the per-launch durations come from the
+        # serialised leg below
+        r = steps_run(steps, not overlap, ktimes)
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
         elapsed = time.perf_counter() - t0
         N, E, C = int(r.n_boxes), int(r.n_edges), int(r.n_cliques)
         V = int(r.n_vert.sum())
+        r = None
+        if overlap:
+            # the roofline's per-launch kernel durations: SER_STEPS steps on one context, one
+            # stream, each launch alone on the GPU (HIP events around every kernel)
+            ktimes = {"__steps": SER_STEPS}
+            for _ in range(SER_STEPS):
+                step(True)
+                for name, ms in ctx.kernel_times():
+                    ktimes[name] = ktimes.get(name, 0.0) + ms
     finally:
         for c in ctxs:
             c.close()
@@ -490,7 +511,8 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
                    "boxes_per_gpu": N, "edges_per_gpu": E, "cliques_per_gpu": C,
                    "parallelism": f"dp{world} (micrograph shards)",
                    "io": "host buffers over PCIe (--host-io)" if host_io else "HBM-resident",
-                   "steps_in_flight": 2 if pipeline else 1},
+                   "steps_in_flight": 2 if pipeline else 1,
+                   "streams": 2 if overlap else 1},
         "edges_per_sec": tot_e * steps / elapsed,
         "totals": {"micrographs": tot_mg, "edges": tot_e, "cliques": tot_c},
         "roofline": {"bound": derived_bound(rec, kind, dom_bytes, dom_ms, dv_kernel),
@@ -505,7 +527,13 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
                          "SURVEY.md 8(d): 28 N + 32 E + C (20 k + 12)",
                      "compulsory_bytes_per_step": fused_compulsory_bytes(N, C, cfg.k, V, n_mg),
                      "kernel_ms_per_step": dom_ms,
-                     "timed_steps": f"HIP events on {nt} of the {steps} timed steps",
+                     # the same bytes over the wall time per step (steps overlapping on two
+                     # streams finish faster than one launch alone)
+                     "frac_step_wall": dom_bytes / (elapsed / steps) / 1e9 / HBM_PEAK_GBS,
+                     "timed_steps": (f"HIP events on {nt} serialised steps (one context, one "
+                                     f"stream) after the {steps} timed steps, which overlap on "
+                                     f"two streams" if overlap else
+                                     f"HIP events on {nt} of the {steps} timed steps"),
                      "kernel_ms_parts": {k_: round(avg[k_], 5) for k_ in ("k_fused", "k_fused_ties")
                                          if k_ in avg} if dom == "k_fused" else None},
         "pipeline": {"device_ms_per_step": dev_ms, "alg_bytes": pipe,
@@ -548,12 +576,19 @@ def main():
                          "pinned host memory inside each step")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="synchronous rgc_run per step instead of two contexts in flight")
+    ap.add_argument("--streams", type=int, choices=(1, 2), default=2,
+                    help="pipelined steps: 2 (default) puts the two contexts on two streams, so "
+                         "step i+1 runs in step i's drain tail; 1 serialises them on one stream "
+                         "(the rocprof evidence command: per-launch durations that do not "
+                         "overlap)")
     ap.add_argument("--by-config", default=None,
                     help="comma-separated by_config entries (BY_CONFIG names) also timed in this "
                          "run (default: every other BASELINE config at its bench size plus "
                          "C4_100k, when --n_mg is not given; 'none' to skip)")
     ap.add_argument("--by-config-cpu-budget", type=float, default=6.0,
                     help="seconds of the 1-core CPU baseline sample per by_config entry (0: none)")
+    ap.add_argument("--no-variants", action="store_true",
+                    help="skip stats_copy_variant (profiling runs: only the headline's launches)")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -570,7 +605,8 @@ def main():
     env = Env(args)
     n_mg = args.n_mg or DEFAULT_MG[args.config]
     rep, cfg, mgs = measure(args, env, args.config, n_mg, args.steps, args.warmup,
-                            host_io=args.host_io, no_pipeline=args.no_pipeline)
+                            host_io=args.host_io, no_pipeline=args.no_pipeline,
+                            streams=args.streams)
     out = {"metric": "micrographs/sec (get_cliques, whole node) at 1/2/4/8 MI355X; % HBM roofline"}
     out.update(rep)
     out.update({"higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -596,7 +632,7 @@ def main():
         for name in extra:
             config, n_c = BY_CONFIG[name]
             r_c, cfg_c, mgs_c = measure(args, env, config, n_c, args.steps, args.warmup,
-                                        no_pipeline=args.no_pipeline)
+                                        no_pipeline=args.no_pipeline, streams=args.streams)
             byc[name] = by_config_entry(r_c)
             if cpu_rank0 and args.by_config_cpu_budget > 0 and not args.no_cpu_baseline:
                 if config not in cpu_of:
@@ -611,11 +647,12 @@ def main():
         out["cpu_baseline"] = cpu_baseline(cfg, mgs, args.cpu_budget, config=args.config)
         if "by_config" in out:
             out["by_config"][args.config]["cpu_baseline"] = out["cpu_baseline"]
-    if not args.host_io and not args.no_pipeline and n_mg == DEFAULT_MG.get(args.config):
+    if (not args.host_io and not args.no_pipeline and not args.no_variants
+            and n_mg == DEFAULT_MG.get(args.config)):
         # the rate with every step's per-micrograph stats copied to the host (what
         # the CLI reads), next to the headline's lazy-stats rate
         r_s, _, _ = measure(args, env, args.config, n_mg, args.steps, args.warmup,
-                            lazy_stats=False)
+                            lazy_stats=False, streams=args.streams)
         out["stats_copy_variant"] = {"value": r_s["value"], "ms_per_step": r_s["ms_per_step"],
                                      "note": "same workload, per-micrograph stats (48 B each) "
                                              "copied to pinned host memory in every step"}

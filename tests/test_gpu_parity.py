@@ -335,11 +335,13 @@ def test_gpu_device_resident_inputs_and_offsets():
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout + r.stderr
 
 
-def test_gpu_submit_wait_pipelined_contexts():
-    """rgc_submit / rgc_wait (ABI 3) on two contexts sharing one stream, the bench's pipelined
-    steps: every batch's outputs equal rgc_run's.  Batches cover the single-launch fast path,
-    a micrograph that needs the f64 pass (the fast path falls back at rgc_wait) and a batch
-    with a large micrograph (general path at rgc_submit).  Child process as above."""
+@pytest.mark.parametrize("streams", [1, 2])
+def test_gpu_submit_wait_pipelined_contexts(streams):
+    """rgc_submit / rgc_wait (ABI 3) on two contexts sharing one stream, or on a stream each
+    (bench.py's default: consecutive steps' launches overlap), the bench's pipelined steps:
+    every batch's outputs equal rgc_run's.  Batches cover the single-launch fast path, a
+    micrograph that needs the f64 pass (the fast path falls back at rgc_wait) and a batch with
+    a large micrograph (general path at rgc_submit).  Child process as above."""
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -347,7 +349,8 @@ def test_gpu_submit_wait_pipelined_contexts():
     env = dict(os.environ, PYTHONPATH=os.pathsep.join(
         [root, os.path.join(root, "repic-copy_amd"), here, os.environ.get("PYTHONPATH", "")]))
     r = subprocess.run([sys.executable, "-c",
-                        "import test_gpu_parity as t; t._submit_wait_check(); print('OK')"],
+                        f"import test_gpu_parity as t; t._submit_wait_check({streams}); "
+                        "print('OK')"],
                        env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout + r.stderr
 
@@ -364,7 +367,7 @@ def _d2h(ptr, n, dtype):
     return out
 
 
-def _submit_wait_check():
+def _submit_wait_check(streams=1):
     import torch
     torch.cuda.init()
 
@@ -407,7 +410,8 @@ def _submit_wait_check():
         dev_in.append(t)
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev).cuda_stream
-    ctxs = [_lib.Context(0, stream), _lib.Context(0, stream)]
+    s2 = torch.cuda.Stream(dev) if streams == 2 else None
+    ctxs = [_lib.Context(0, stream), _lib.Context(0, s2.cuda_stream if s2 else stream)]
 
     def submit(c, i, lazy=False):
         # lazy: ABI 6 F_LAZY_STATS (the bench's steps): per-micrograph outputs fetched from HBM

@@ -1,7 +1,9 @@
 #!/bin/bash
 # Measurement evidence per config: the bench line with its CPU baseline,
-# rocprofv3 --kernel-trace --stats of the same command, and the PMC passes whose traffic /
-# counters bench.py folds into roofline.traffic / limiter (tools/gpu_pmc.sh).
+# rocprofv3 --kernel-trace --stats of the same bench with its steps serialised on one stream
+# (--streams 1: per-launch durations that do not overlap, as the default line's roofline leg
+# times them), and the PMC passes whose traffic / counters bench.py folds into roofline.traffic
+# / limiter (tools/gpu_pmc.sh).
 #   gpurun --timeout 1200 -- bash tools/gpu_evidence.sh TAG "C2 C3 C4 C5"
 set -e -o pipefail
 TAG=${1:-ev}; CFGS=${2:-"C2 C3 C4 C5"}
@@ -11,7 +13,7 @@ export TMPDIR=/tmp
 for C in $CFGS; do
   echo "== $C stats"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$C" -o run -- \
-    python3 bench.py --config $C --no-cpu-baseline --by-config none > "$OUT/bench_prof_$C.json" 2> "$OUT/prof_$C.err" \
+    python3 bench.py --config $C --no-cpu-baseline --by-config none --streams 1 --no-variants > "$OUT/bench_prof_$C.json" 2> "$OUT/prof_$C.err" \
     || { tail -30 "$OUT/prof_$C.err"; exit 1; }
   find "$OUT/prof_$C" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats_$C.csv" \;
   head -8 "$OUT/kernel_stats_$C.csv"

@@ -11,7 +11,7 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 STEPS=3; WARM=1
-BENCH=(python3 bench.py --no-cpu-baseline --by-config none --steps $STEPS --warmup $WARM --config "$CFG")
+BENCH=(python3 bench.py --no-cpu-baseline --by-config none --streams 1 --no-variants --steps $STEPS --warmup $WARM --config "$CFG")
 if [ -n "$NMG" ]; then BENCH+=(--n_mg "$NMG"); fi
 KSUB="k_fused<"
 if [ "$CFG" = "C5" ]; then KSUB=rgc::; fi
