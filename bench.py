@@ -35,8 +35,10 @@ DEFAULT_MG = {"C2": 10000, "C3": 4000, "C4": 12500, "C5": 64}
 # by_config entries: name -> (BASELINE config, micrographs per GPU).  C4_100k is the north-star
 # batch (BASELINE configs[3]: 100k micrographs, 5 pickers) on ONE GPU, the 1-GPU point of the
 # 1 -> 8 curve; C4 is its 12.5k-micrograph per-GPU shard at 8 GPUs.
+# C5_256: the large-micrograph route at 256 micrographs per step (its per-micrograph kernels,
+# one workgroup per micrograph, fill 64 of 256 CUs at C5's 64 per step)
 BY_CONFIG = {"C2": ("C2", 10000), "C3": ("C3", 4000), "C4": ("C4", 12500), "C5": ("C5", 64),
-             "C4_100k": ("C4", 100000)}
+             "C4_100k": ("C4", 100000), "C5_256": ("C5", 256)}
 
 
 def fused_compulsory_bytes(N, C, k, V, n_mg):
@@ -619,7 +621,7 @@ def main():
     # C4 at the 100k / 8-GPU shard of 12.5k micrographs per GPU, C4_100k the whole north-star
     # batch on this GPU), each with a 1-core CPU baseline sample on rank 0
     if args.by_config is None:
-        extra = [] if args.n_mg else [c for c in ("C2", "C3", "C4", "C5", "C4_100k")
+        extra = [] if args.n_mg else [c for c in ("C2", "C3", "C4", "C5", "C4_100k", "C5_256")
                                       if c != args.config]
     elif args.by_config.lower() == "none":
         extra = []
