@@ -20,6 +20,7 @@
 #include <string>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -218,6 +219,10 @@ struct rgc_ctx {
   rgc_batch_out pend_out{};
   hipEvent_t ev_sub = nullptr;   // after the submitted run's stats copy
   int qg_nslots = 0;             // HBM level-tree slots allocated (ensure_qg)
+  uint32_t tiles_epoch = 0;      // scan_epoch_count() when D_TILES was last zeroed
+  // rgc_submit's general path (host syncs per clique level) runs here; rgc_wait joins it
+  std::thread worker;
+  std::string pend_err;          // the worker's error message (g_err is per thread)
 };
 
 static int ensure_dev(rgc_ctx* c, int id, size_t bytes, size_t keep = 0) {
@@ -235,9 +240,23 @@ static int ensure_dev(rgc_ctx* c, int id, size_t bytes, size_t keep = 0) {
   if (b.p) HIPCHK(hipFree(b.p));
   b.p = p;
   b.cap = cap;
-  // the scan tile buffer's word 0 is the one-pass scan's claim counter: zero in a new buffer
-  // (every scan leaves it zero)
-  if (id == D_TILES) HIPCHK(hipMemsetAsync(p, 0, 64, c->stream));
+  // the scan tile buffer: word 0 is the one-pass scan's claim counter (every scan leaves it
+  // zero), the rest per-tile states tagged with a launch epoch; a new buffer starts all zero
+  // (no state of a reused allocation can match a later epoch)
+  if (id == D_TILES) {
+    HIPCHK(hipMemsetAsync(p, 0, cap, c->stream));
+    c->tiles_epoch = scan_epoch_count();
+  }
+  return 0;
+}
+
+// Before a run that scans: launch epochs repeat after 2^22 - 1 scans process-wide, so a tile
+// buffer whose states may date from SCAN_EPOCH_REFRESH scans ago is zeroed first.
+static int tiles_refresh(rgc_ctx* c) {
+  Buf& b = c->d[D_TILES];
+  if (!b.p || scan_epoch_count() - c->tiles_epoch < SCAN_EPOCH_REFRESH) return 0;
+  HIPCHK(hipMemsetAsync(b.p, 0, b.cap, c->stream));
+  c->tiles_epoch = scan_epoch_count();
   return 0;
 }
 
@@ -636,6 +655,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
   const bool want_members = (flags & (RGC_F_MEMBERS | RGC_F_MULTI_OUT)) != 0;
   const bool want_edges = (flags & RGC_F_EDGES) != 0;
   c->n_edge_dump = 0;
+  TRY(tiles_refresh(c));
   const double B = (double)in->box_size;
   const double two_b2 = (double)(2 * in->box_size * in->box_size);
   c->timing = (flags & RGC_F_TIMING) != 0;
@@ -1284,6 +1304,7 @@ int rgc_ctx_create(int device, void* hip_stream, rgc_ctx** out) {
 
 void rgc_ctx_destroy(rgc_ctx* c) {
   if (!c) return;
+  if (c->worker.joinable()) c->worker.join();
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& b : c->d)
@@ -1320,7 +1341,24 @@ int rgc_submit(rgc_ctx* c, const rgc_batch_in* in) {
   if (r < 0) return r;
   c->pend = true;
   c->pend_fast = r == 1;
-  if (!c->pend_fast) c->pend_rc = run_impl(c, in, &c->pend_out);   // general path, now
+  if (!c->pend_fast) {
+    // the general path syncs on the host once per clique level: on a worker thread, so the
+    // caller's next submit (another context, another stream) overlaps this run's device work
+    // and its host round trips; rgc_wait joins it.  (No thread: the run happens here.)
+    try {
+      c->worker = std::thread([c] {
+        if (hipSetDevice(c->device) != hipSuccess) {
+          c->pend_rc = fail("hipSetDevice failed on the submit worker");
+        } else {
+          c->pend_rc = run_impl(c, &c->pin, &c->pend_out);
+        }
+        if (c->pend_rc != 0) c->pend_err = g_err;
+      });
+    } catch (...) {
+      c->pend_rc = run_impl(c, &c->pin, &c->pend_out);
+      if (c->pend_rc != 0) c->pend_err = g_err;
+    }
+  }
   return 0;
 }
 
@@ -1330,7 +1368,9 @@ int rgc_wait(rgc_ctx* c, rgc_batch_out* out) {
   HIPCHK(hipSetDevice(c->device));
   c->pend = false;
   if (!c->pend_fast) {
+    if (c->worker.joinable()) c->worker.join();
     *out = c->pend_out;
+    if (c->pend_rc != 0) g_err = c->pend_err;
     return c->pend_rc;
   }
   const int r = wait_fast(c, out);
@@ -1534,6 +1574,7 @@ int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) 
   TRY(ensure_dev(c, D_IL_X, nc));
   TRY(ensure_dev(c, D_IL_EX, nc));
   TRY(ensure_dev(c, D_TILES, scan_tiles_needed(std::max(nc, nr) + 1) * 8));
+  TRY(tiles_refresh(c));
   TRY(ensure_dev(c, D_TOTAL, 32));
   TRY(ensure_host(c, H_TOTAL, 64));
   HIPCHK(hipMemcpyAsync(c->d[D_IL_CPTR].p, in->col_ptr, (nc + 1) * 8, hipMemcpyHostToDevice, s));

@@ -222,6 +222,11 @@ struct FillSegs {
 };
 void launch_fill_multi(hipStream_t stream, const FillSegs& F);
 int64_t scan_tiles_needed(int64_t n);
+// one-pass scan launches so far (process-wide); a tile buffer whose states are older than
+// SCAN_EPOCH_REFRESH launches must be zeroed before its next scan (launch epochs repeat after
+// 2^22 - 1 launches)
+constexpr uint32_t SCAN_EPOCH_REFRESH = 1u << 20;
+uint32_t scan_epoch_count();
 void launch_scan(hipStream_t stream, int64_t n, const int32_t* in, int64_t* out,
                  int64_t* tile_buf, int64_t* total);
 void launch_cc(hipStream_t stream, int phase, int N, int n_mg, int k, int get_cc,

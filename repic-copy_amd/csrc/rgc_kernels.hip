@@ -943,12 +943,12 @@ void launch_bin(hipStream_t stream, int n_mg, int k, double B, const int32_t* bo
   const int lds = (wide ? 4 * keys : 2 * (keys + 2)) + 16;
   if (wide) {
     static std::atomic<uint64_t> attr{0};
-    set_dyn_lds_once(attr, reinterpret_cast<const void*>(&k1_bin<true>), 132 * 1024);
+    (void)set_dyn_lds_once(attr, reinterpret_cast<const void*>(&k1_bin<true>), 132 * 1024);
     hipLaunchKernelGGL(k1_bin<true>, dim3(n_mg), dim3(1024), lds, stream, k, B, box_off,
                        cell_off, x, y, grid, cell_start, sx, sy, sbox, spick, smg, bmg, bpick);
   } else {
     static std::atomic<uint64_t> attr{0};
-    set_dyn_lds_once(attr, reinterpret_cast<const void*>(&k1_bin<false>), 132 * 1024);
+    (void)set_dyn_lds_once(attr, reinterpret_cast<const void*>(&k1_bin<false>), 132 * 1024);
     hipLaunchKernelGGL(k1_bin<false>, dim3(n_mg), dim3(1024), lds, stream, k, B, box_off,
                        cell_off, x, y, grid, cell_start, sx, sy, sbox, spick, smg, bmg, bpick);
   }
@@ -973,6 +973,9 @@ void launch_pairs(hipStream_t stream, bool fill, int N, int k, double B, double 
 // scan's tile sums fit the same words)
 int64_t scan_tiles_needed(int64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 2; }
 
+static std::atomic<uint32_t> g_scan_epochs{0};
+uint32_t scan_epoch_count() { return g_scan_epochs.load(); }
+
 void launch_scan(hipStream_t stream, int64_t n, const int32_t* in, int64_t* out,
                  int64_t* tile_buf, int64_t* total) {
 #ifdef RGC_X_SCAN3   // the three-launch scan (A/B timing)
@@ -982,9 +985,10 @@ void launch_scan(hipStream_t stream, int64_t n, const int32_t* in, int64_t* out,
   if (nt > 0) RGC_LAUNCH(scan_apply, nt, WG, n, in, tile_buf + 1, total, out);
   else (void)hipMemcpyAsync(out, total, sizeof(int64_t), hipMemcpyDeviceToDevice, stream);
 #else
-  // launch epochs are process-wide (any two launches sharing a tile buffer differ)
-  static std::atomic<uint32_t> epochs{0};
-  const uint32_t e = epochs.fetch_add(1) % ((1u << 22) - 1) + 1;
+  // launch epochs are process-wide (any two launches sharing a tile buffer differ; an epoch
+  // repeats after 2^22 - 1 launches, so the owner of a tile buffer zeroes it at least every
+  // SCAN_EPOCH_REFRESH launches: scan_epoch_count)
+  const uint32_t e = g_scan_epochs.fetch_add(1) % ((1u << 22) - 1) + 1;
   const int64_t nt = std::max<int64_t>(1, (n + ONE_TILE - 1) / ONE_TILE);
   RGC_LAUNCH(scan_onepass, nt, WG, n, in, out, total, reinterpret_cast<uint64_t*>(tile_buf), e);
 #endif
