@@ -126,9 +126,12 @@ int rgc_run(rgc_ctx* ctx, const rgc_batch_in* in, rgc_batch_out* out);
  * as rgc_run would.  Host and device arrays of the batch must stay valid until rgc_wait.  A
  * batch that takes the single fused launch (HBM-resident inputs and offsets, RGC_F_DEVICE_INPUTS
  * | RGC_F_DEVICE_META, device outputs) runs while the caller continues, so with two contexts
- * on one stream the host prepares and launches batch i+1 while the device runs batch i; any
- * other batch (or one whose micrographs need a second pass) runs through rgc_run's general
- * path.  Outputs stay valid until the next submit/run on the same context.  While a submitted
+ * on one stream the host prepares and launches batch i+1 while the device runs batch i (on
+ * two streams the two launches also overlap on the device); any other batch runs through
+ * rgc_run's general path on a worker thread of the context (since round 5: it syncs on the
+ * host once per clique level, so a second context on its own stream keeps the device busy
+ * meanwhile), and one whose micrographs need a second pass re-runs that path inside rgc_wait.
+ * Outputs stay valid until the next submit/run on the same context.  While a submitted
  * run awaits rgc_wait, rgc_submit, rgc_run, rgc_score_pairs and rgc_ilp_solve on the same
  * context fail (negative return, rgc_last_error says why). */
 int rgc_submit(rgc_ctx* ctx, const rgc_batch_in* in);
