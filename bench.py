@@ -321,6 +321,7 @@ class Env:
         self.local = int(os.environ.get("RGC_BENCH_DEVICE", local))
         self.backend = os.environ.get("RGC_DIST_BACKEND", "nccl")
         self.dist = None
+        self.streams = None   # measure(): the two library streams, created on first use
         if self.world > 1:
             import torch.distributed as dist
             torch.cuda.set_device(self.local)
@@ -375,7 +376,10 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
     # one explicit stream for every context (torch's default stream handle is 0, with which
     # each context would create its own stream, and two in-flight steps would run their
     # kernels concurrently: more throughput, but per-launch kernel times that overlap)
-    tstream = torch.cuda.Stream(dev)
+    # (the process's two streams, created once: every measure() runs on the same pair)
+    if env.streams is None:
+        env.streams = (torch.cuda.Stream(dev), torch.cuda.Stream(dev))
+    tstream, tstream2 = env.streams
     stream = tstream.cuda_stream
     ctx = _lib.Context(env.local, stream)
     flags = _lib.F_DEVICE_INPUTS
@@ -386,7 +390,6 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
     # step i+1's workgroups fill the CUs step i's drain tail leaves idle
     pipeline = not (host_io or no_pipeline)
     if pipeline and streams == 2:
-        tstream2 = torch.cuda.Stream(dev)
         ctxs = [ctx, _lib.Context(env.local, tstream2.cuda_stream)]
     else:
         ctxs = [ctx, _lib.Context(env.local, stream)] if pipeline else [ctx]
