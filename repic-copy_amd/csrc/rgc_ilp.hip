@@ -30,6 +30,10 @@ constexpr uint8_t ST_IN_SEED = 1;        // (= ST_IN below: the pre-search packi
 constexpr uint8_t ILP_UNSEARCHED = 255;  // wave component skipped past the time budget
 constexpr int ILP_SMALL = 64;     // thread-per-component limit (one 64-bit mask)
 constexpr int ILP_BIG = 4096;     // wave-per-component limit (64 lanes x 64 bits)
+// the wave search stops at Gurobi's MIPGap (GAP_OK) only after this many nodes: a component
+// whose search proves optimality sooner gets its exact optimum (status OPTIMAL), as an exact
+// solver's choice, and only the hard ones take the 1e-4 early stop
+constexpr int64_t ILP_GAP_NODES = 1 << 16;
 
 __device__ __forceinline__ int32_t ilp_find(int32_t* p, int32_t x) {
   for (;;) {
@@ -490,18 +494,26 @@ __global__ __launch_bounds__(64) void k_ilp_wave(IlpArgs A, int n_big) {
     for (; status == RGC_ILP_OPTIMAL;) {
       bool back = false;
       if (++nodes > node_cap) { status = RGC_ILP_NODE_LIMIT; break; }
-      // the launch's time budget, checked every 1024 nodes
-      if (deadline && (nodes & 1023) == 0 &&
-          (uint64_t)__builtin_amdgcn_s_memrealtime() > deadline) {
-        status = RGC_ILP_NODE_LIMIT;
-        break;
+      // the launch's time budget, and past ILP_GAP_NODES the MIPGap stop, every 1024 nodes
+      if ((nodes & 1023) == 0) {
+        if (deadline && (uint64_t)__builtin_amdgcn_s_memrealtime() > deadline) {
+          status = RGC_ILP_NODE_LIMIT;
+          break;
+        }
+        if (nodes >= ILP_GAP_NODES && best > 0.0 && root_bound - best <= 1e-4 * best) {
+          status = RGC_ILP_GAP_OK;
+          break;
+        }
       }
       const uint64_t nz = __ballot(P != 0);
       if (nz == 0) {
         if (cur > best) {
           best = cur;
           best_set = chosen;
-          if (root_bound - best <= 1e-4 * best && depth > 0) { status = RGC_ILP_GAP_OK; break; }
+          if (nodes >= ILP_GAP_NODES && root_bound - best <= 1e-4 * best && depth > 0) {
+            status = RGC_ILP_GAP_OK;
+            break;
+          }
         }
         back = true;
       } else if ((lag && cur + lag_bound(P) <= best) || cur + bound(P) <= best) {
