@@ -306,6 +306,10 @@ def derived_bound(rec, kernel, alg_bytes, kernel_ms, dv_kernel="k_fused"):
 
 TIME_EVERY = 4   # pipelined steps: one in TIME_EVERY carries the HIP timing events
 SER_STEPS = 8    # two-stream runs: serialised steps timed with HIP events for the roofline
+# steps in flight (contexts, one stream each): the large route (C5) syncs on the host once per
+# clique level, so a third step in flight keeps the device busier (C5 -3 % against two); the
+# fused configs lose 3-4 % at three (profiles/r05u_ab_depth3.txt)
+PIPE_DEPTH = {"C5": 3}
 
 
 class Env:
@@ -336,7 +340,7 @@ class Env:
 
 
 def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=False,
-            lazy_stats=True, streams=1):
+            lazy_stats=True, streams=1, depth=None):
     """Time ``steps`` steps of the hot path over one synthetic batch of ``config`` (n_mg
     micrographs per rank, inputs resident in HBM): barrier + synchronize on both sides, max
     over ranks.  Returns (report dict, cfg, this rank's micrographs)."""
@@ -346,6 +350,7 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
     from repic_amd.pipeline import Batch
 
     dist, world, rank, dev, cdev = env.dist, env.world, env.rank, env.dev, env.cdev
+    depth = depth or PIPE_DEPTH.get(config, 2)
     cfg = synth.SynthConfig(**synth.CONFIGS[config], seed=args.seed)
     t_gen = time.time()
     # this rank's shard of one big batch (identical to packing synth.batch's list; large
@@ -378,8 +383,10 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
     # kernels concurrently: more throughput, but per-launch kernel times that overlap)
     # (the process's two streams, created once: every measure() runs on the same pair)
     if env.streams is None:
-        env.streams = (torch.cuda.Stream(dev), torch.cuda.Stream(dev))
-    tstream, tstream2 = env.streams
+        env.streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    while len(env.streams) < depth:   # (experiments: tools/streams_ab.py --depth)
+        env.streams.append(torch.cuda.Stream(dev))
+    tstream = env.streams[0]
     stream = tstream.cuda_stream
     ctx = _lib.Context(env.local, stream)
     flags = _lib.F_DEVICE_INPUTS
@@ -390,7 +397,8 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
     # step i+1's workgroups fill the CUs step i's drain tail leaves idle
     pipeline = not (host_io or no_pipeline)
     if pipeline and streams == 2:
-        ctxs = [ctx, _lib.Context(env.local, tstream2.cuda_stream)]
+        ctxs = [ctx] + [_lib.Context(env.local, env.streams[j].cuda_stream)
+                        for j in range(1, depth)]
     else:
         ctxs = [ctx, _lib.Context(env.local, stream)] if pipeline else [ctx]
 
@@ -429,14 +437,16 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
         def timed(i):
             return timing and i % TIME_EVERY == 0
 
-        submit(ctxs[0], timed(0))
+        nd = len(ctxs)   # steps in flight
+        for j in range(min(nd - 1, n)):
+            submit(ctxs[j], timed(j))
         for i in range(n):
             # drop step i-1's Result before its context is reused: a Result still referenced
             # at the next submit makes the context hand its host buffers over to it
             r = None
-            if i + 1 < n:
-                submit(ctxs[(i + 1) % 2], timed(i + 1))
-            c = ctxs[i % 2]
+            if i + nd - 1 < n:
+                submit(ctxs[(i + nd - 1) % nd], timed(i + nd - 1))
+            c = ctxs[i % nd]
             r = c.wait()
             if ktimes is not None and timed(i):
                 ktimes["__steps"] = ktimes.get("__steps", 0) + 1
@@ -516,8 +526,8 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
                    "boxes_per_gpu": N, "edges_per_gpu": E, "cliques_per_gpu": C,
                    "parallelism": f"dp{world} (micrograph shards)",
                    "io": "host buffers over PCIe (--host-io)" if host_io else "HBM-resident",
-                   "steps_in_flight": 2 if pipeline else 1,
-                   "streams": 2 if overlap else 1},
+                   "steps_in_flight": len(ctxs) if pipeline else 1,
+                   "streams": len(ctxs) if overlap else 1},
         "edges_per_sec": tot_e * steps / elapsed,
         "totals": {"micrographs": tot_mg, "edges": tot_e, "cliques": tot_c},
         "roofline": {"bound": derived_bound(rec, kind, dom_bytes, dom_ms, dv_kernel),
@@ -537,7 +547,7 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
                      "frac_step_wall": dom_bytes / (elapsed / steps) / 1e9 / HBM_PEAK_GBS,
                      "timed_steps": (f"HIP events on {nt} serialised steps (one context, one "
                                      f"stream) after the {steps} timed steps, which overlap on "
-                                     f"two streams" if overlap else
+                                     f"{len(ctxs)} streams" if overlap else
                                      f"HIP events on {nt} of the {steps} timed steps"),
                      "kernel_ms_parts": {k_: round(avg[k_], 5) for k_ in ("k_fused", "k_fused_ties")
                                          if k_ in avg} if dom == "k_fused" else None},

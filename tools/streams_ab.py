@@ -21,21 +21,26 @@ def main():
     ap.add_argument("configs", nargs="+")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--depth", type=int, default=0,
+                    help="also time DEPTH contexts in flight, each on its own stream")
     a = ap.parse_args()
     args = argparse.Namespace(seed=0)
     env = bench.Env(args)
     for name in a.configs:
         config, n_mg = bench.BY_CONFIG[name]
-        ms = {1: [], 2: []}
+        legs = [(1, 2), (2, 2)] + ([(2, a.depth)] if a.depth > 2 else [])
+        ms = {lg: [] for lg in legs}
         for _ in range(a.rounds):
-            for s in (1, 2):
-                rep, _, _ = bench.measure(args, env, config, n_mg, a.steps, 4, streams=s)
-                ms[s].append(rep["ms_per_step"])
-        m1, m2 = statistics.median(ms[1]), statistics.median(ms[2])
+            for s_, d_ in legs:
+                rep, _, _ = bench.measure(args, env, config, n_mg, a.steps, 4, streams=s_,
+                                          depth=d_)
+                ms[(s_, d_)].append(rep["ms_per_step"])
+        m1 = statistics.median(ms[(1, 2)])
         print(f"{name} {n_mg} micrographs: wall ms per step (median of {a.rounds}, interleaved)")
-        print(f"  one stream      {m1:8.4f} ms   {ms[1]}")
-        print(f"  two streams     {m2:8.4f} ms   {ms[2]}   ({(m2 / m1 - 1) * 100:+.1f} %)",
-              flush=True)
+        for (s_, d_), v in ms.items():
+            m = statistics.median(v)
+            label = "one stream" if s_ == 1 else f"{d_} streams"
+            print(f"  {label:14s}  {m:8.4f} ms   {v}   ({(m / m1 - 1) * 100:+.1f} %)", flush=True)
 
 
 if __name__ == "__main__":
