@@ -300,8 +300,10 @@ class Context:
                dev_meta=None):
         """``run`` without waiting (rgc_submit): the batch is enqueued on the context's stream
         and :meth:`wait` returns its :class:`Result`.  One submission in flight per context;
-        two contexts on one stream overlap the host side of batch i+1 with the device work of
-        batch i.  The arrays passed in must stay alive until ``wait`` (kept here)."""
+        two contexts overlap the host side of batch i+1 with the device work of batch i, and on
+        two streams also the two batches' kernels (bench.py's default).  A batch that needs the
+        general path (large micrographs) runs on the context's worker thread until ``wait``.
+        The arrays passed in must stay alive until ``wait`` (kept here)."""
         bi, keep, flags = self._batch_in(n_mg, k, box_size, box_off, id_base, x, y, score, flags,
                                          dev_meta)
         self._retire()
