@@ -339,6 +339,35 @@ class Env:
         self.cdev = self.dev if self.backend == "nccl" else torch.device("cpu")
 
 
+def pipelined_steps(ctxs, submit, n, timing, ktimes=None):
+    """n steps over the contexts round-robin with len(ctxs) of them in flight: step i is
+    submitted on ctxs[i % d] once step i - d + 1 has been waited for (d = len(ctxs)); returns
+    the last step's Result.  ``submit(ctx, timed)`` enqueues one step.  HIP timing events cost
+    ~5 us of idle GPU each between launches (tools/step_gap.py: ~15 us per C2 step with the
+    three per step), so with ``timing`` every TIME_EVERY-th step carries them and ``ktimes``
+    sums those steps' kernel times (count in "__steps")."""
+    def timed(i):
+        return timing and i % TIME_EVERY == 0
+
+    nd = len(ctxs)
+    r = None
+    for j in range(min(nd - 1, n)):
+        submit(ctxs[j], timed(j))
+    for i in range(n):
+        # drop step i-1's Result before its context is reused: a Result still referenced at
+        # the next submit makes the context hand its host buffers over to it
+        r = None
+        if i + nd - 1 < n:
+            submit(ctxs[(i + nd - 1) % nd], timed(i + nd - 1))
+        c = ctxs[i % nd]
+        r = c.wait()
+        if ktimes is not None and timed(i):
+            ktimes["__steps"] = ktimes.get("__steps", 0) + 1
+            for name, ms in c.kernel_times():
+                ktimes[name] = ktimes.get(name, 0.0) + ms
+    return r
+
+
 def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=False,
             lazy_stats=True, streams=1, depth=None):
     """Time ``steps`` steps of the hot path over one synthetic batch of ``config`` (n_mg
@@ -431,28 +460,7 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
                     for name, ms in ctx.kernel_times():
                         ktimes[name] = ktimes.get(name, 0.0) + ms
             return r
-        # HIP timing events cost ~5 us of idle GPU each between launches (tools/step_gap.py:
-        # ~15 us per C2 step with the three per step), so in the pipelined loop every
-        # TIME_EVERY-th step carries them; the per-kernel averages are over those steps
-        def timed(i):
-            return timing and i % TIME_EVERY == 0
-
-        nd = len(ctxs)   # steps in flight
-        for j in range(min(nd - 1, n)):
-            submit(ctxs[j], timed(j))
-        for i in range(n):
-            # drop step i-1's Result before its context is reused: a Result still referenced
-            # at the next submit makes the context hand its host buffers over to it
-            r = None
-            if i + nd - 1 < n:
-                submit(ctxs[(i + nd - 1) % nd], timed(i + nd - 1))
-            c = ctxs[i % nd]
-            r = c.wait()
-            if ktimes is not None and timed(i):
-                ktimes["__steps"] = ktimes.get("__steps", 0) + 1
-                for name, ms in c.kernel_times():
-                    ktimes[name] = ktimes.get(name, 0.0) + ms
-        return r
+        return pipelined_steps(ctxs, submit, n, timing, ktimes)
 
     overlap = pipeline and streams == 2
     try:

@@ -58,3 +58,51 @@ def test_roofline_bound_follows_the_counters():
     assert bench.derived_bound({"step_traffic": 2e9}, "route", 8e9, 8.0, "k5l") == "unmeasured"
     route = {"step_traffic": 2e9, "kernels": {"k5_epilogue": {"derived": {"valu_busy": 0.7}}}}
     assert bench.derived_bound(route, "route", 8e9, 8.0, "k5_epilogue") == "valu"
+
+
+class _StubCtx:
+    """submit / wait bookkeeping of one library context (one run in flight, as rgc_submit)"""
+
+    def __init__(self, name, log):
+        self.name, self.log, self.pending = name, log, None
+
+    def submit(self, step, timed):
+        assert self.pending is None, "submit on a context with a run in flight"
+        self.pending = (step, timed)
+        self.log.append(("submit", self.name, step))
+
+    def wait(self):
+        assert self.pending is not None, "wait without a submission"
+        step, timed = self.pending
+        self.pending = None
+        self.log.append(("wait", self.name, step))
+        return ("result", step)
+
+    def kernel_times(self):
+        return [("k_fused", 1.0)] if self.pending is None else []
+
+
+@pytest.mark.parametrize("depth,n", [(1, 5), (2, 7), (3, 7), (3, 2), (2, 1)])
+def test_pipelined_steps_order_and_depth(depth, n):
+    """bench.pipelined_steps: steps in order, at most ``depth`` in flight, each context waited
+    for before it is reused, the last step's result returned, timing on every TIME_EVERY-th."""
+    log = []
+    ctxs = [_StubCtx(f"c{j}", log) for j in range(depth)]
+    count = iter(range(10 ** 6))
+
+    def submit(c, timed):
+        c.submit(next(count), timed)
+
+    kt = {}
+    r = bench.pipelined_steps(ctxs, submit, n, True, kt)
+    assert r == ("result", n - 1)
+    subs = [e for e in log if e[0] == "submit"]
+    waits = [e for e in log if e[0] == "wait"]
+    assert [e[2] for e in subs] == list(range(n)) and [e[2] for e in waits] == list(range(n))
+    assert all(e[1] == f"c{e[2] % depth}" for e in subs + waits)
+    in_flight = 0
+    for e in log:
+        in_flight += 1 if e[0] == "submit" else -1
+        assert 0 <= in_flight <= depth
+    assert in_flight == 0
+    assert kt.get("__steps", 0) == len(range(0, n, bench.TIME_EVERY))
