@@ -622,3 +622,45 @@ def _lazy_survive_check():
     assert len(ra.clique_cnt) == a.n_mg and (ra.clique_cnt == want).all(), (ra.clique_cnt, want)
     assert len(rb.clique_cnt) == b.n_mg and (rb.clique_cnt > 0).all()
     ctx.close()
+
+
+def test_gpu_submit_worker_error_and_reuse():
+    """A batch on rgc_submit's general path runs on the context's worker thread: its error
+    (box_size above 2^26) comes back from rgc_wait with the worker's message, and the context
+    then runs further submissions (general path: a micrograph too large for the fused kernel)
+    with outputs equal to rgc_run's."""
+    from repic_amd import _lib, synth
+    from repic_amd.pipeline import Batch
+    cfg = synth.SynthConfig(**synth.CONFIGS["C2"], seed=31)
+    big = synth.SynthConfig(k=3, n_true=1800, box=60, width=4096, height=4096, keep=0.9,
+                            jit=0.08, fp=0.1, seed=32)
+    b = Batch.pack(3, 180, synth.batch(cfg, 5) + synth.batch(big, 1))
+    fl = _lib.F_HOST_OUTPUTS | _lib.F_MEMBERS
+    ctx = _lib.Context(0)
+    try:
+        ctx.submit(b.n_mg, 3, 1 << 27, b.box_off, b.id_base, b.x, b.y, b.score, fl)
+        with pytest.raises(_lib.RGCError, match="box_size"):
+            ctx.wait()
+        def snap(r):
+            # micrograph ranges are reserved atomically (their order varies); the content of
+            # each range is deterministic
+            d = {f: np.array(getattr(r, f)) for f in ("status", "clique_cnt")}
+            for f in ("rows", "w", "conf", "consensus", "members"):
+                v = np.asarray(getattr(r, f))
+                d[f] = [v[int(b0):int(b0) + int(n)].copy()
+                        for b0, n in zip(r.clique_base, r.clique_cnt)]
+            return d
+
+        want = snap(ctx.run(b.n_mg, 3, 180, b.box_off, b.id_base, b.x, b.y, b.score, fl))
+        for _ in range(2):
+            ctx.submit(b.n_mg, 3, 180, b.box_off, b.id_base, b.x, b.y, b.score, fl)
+            got = snap(ctx.wait())
+            for f, v in want.items():
+                if isinstance(v, list):
+                    assert len(got[f]) == len(v)
+                    for a, e in zip(got[f], v):
+                        np.testing.assert_array_equal(a, e, err_msg=f)
+                else:
+                    np.testing.assert_array_equal(got[f], v, err_msg=f)
+    finally:
+        ctx.close()
