@@ -11,9 +11,10 @@ ranks (weak scaling, no collective in the hot path).
 
 Prints ONE JSON line on rank 0 (driver contract), with "roofline" (dominant kernel, HIP
 events around each launch) and "cpu_baseline" (the oracle's faithful per-pair loop on a
-bounded sample, 1 core).  Steps are pipelined on two contexts, by default on two streams so
-that step i+1's workgroups run in step i's drain tail (--streams 1 serialises them); the
-roofline's per-launch durations then come from serialised steps timed after the timed region.
+bounded sample, 1 core).  Steps are pipelined on three contexts, each on its own stream, so
+that step i+1's workgroups run in step i's drain tail (--streams 1 serialises two contexts on
+one stream); the roofline's per-launch durations then come from serialised steps timed after
+the timed region.
 """
 from __future__ import annotations
 
@@ -306,10 +307,11 @@ def derived_bound(rec, kernel, alg_bytes, kernel_ms, dv_kernel="k_fused"):
 
 TIME_EVERY = 4   # pipelined steps: one in TIME_EVERY carries the HIP timing events
 SER_STEPS = 8    # two-stream runs: serialised steps timed with HIP events for the roofline
-# steps in flight (contexts, one stream each): the large route (C5) syncs on the host once per
-# clique level, so a third step in flight keeps the device busier (C5 -3 % against two); the
-# fused configs lose 3-4 % at three (profiles/r05u_ab_depth3.txt)
-PIPE_DEPTH = {"C5": 3}
+# steps in flight (contexts, one stream each): three against two, with each run's stats copy
+# on its own launch stream, C2 -1.5 %, C4 -1.3 %, C3 -0.6 %, C5 -4.7 % (the large route syncs
+# on the host once per clique level; profiles/r05w_ab_copy_on_stream.txt)
+PIPE_DEPTH_DEFAULT = 3
+PIPE_DEPTH = {}
 
 
 class Env:
@@ -379,7 +381,7 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
     from repic_amd.pipeline import Batch
 
     dist, world, rank, dev, cdev = env.dist, env.world, env.rank, env.dev, env.cdev
-    depth = depth or PIPE_DEPTH.get(config, 2)
+    depth = depth or PIPE_DEPTH.get(config, PIPE_DEPTH_DEFAULT)
     cfg = synth.SynthConfig(**synth.CONFIGS[config], seed=args.seed)
     t_gen = time.time()
     # this rank's shard of one big batch (identical to packing synth.batch's list; large
@@ -410,7 +412,7 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
     # one explicit stream for every context (torch's default stream handle is 0, with which
     # each context would create its own stream, and two in-flight steps would run their
     # kernels concurrently: more throughput, but per-launch kernel times that overlap)
-    # (the process's two streams, created once: every measure() runs on the same pair)
+    # (the process's streams, created once: every measure() runs on the same ones)
     if env.streams is None:
         env.streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
     while len(env.streams) < depth:   # (experiments: tools/streams_ab.py --depth)
@@ -419,11 +421,11 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
     stream = tstream.cuda_stream
     ctx = _lib.Context(env.local, stream)
     flags = _lib.F_DEVICE_INPUTS
-    # pipelined steps (default): two contexts on that one stream, rgc_submit / rgc_wait, so the
-    # host side of step i+1 (planning, launch) overlaps the device work of step i while the
-    # kernels stay serialised; every step runs the whole hot path into its own context's
-    # outputs and is waited for.  streams=2: the second context on a stream of its own, so
-    # step i+1's workgroups fill the CUs step i's drain tail leaves idle
+    # pipelined steps (default): `depth` contexts in flight (rgc_submit / rgc_wait), so the host
+    # side of step i+1 (planning, launch) overlaps the device work of step i; every step runs
+    # the whole hot path into its own context's outputs and is waited for.  streams=2 (default):
+    # each context on a stream of its own, so step i+1's workgroups fill the CUs step i's
+    # drain tail leaves idle; streams=1: two contexts on one stream, kernels serialised
     pipeline = not (host_io or no_pipeline)
     if pipeline and streams == 2:
         ctxs = [ctx] + [_lib.Context(env.local, env.streams[j].cuda_stream)
@@ -598,12 +600,12 @@ def main():
                          "offsets are uploaded and every per-clique output is copied back to "
                          "pinned host memory inside each step")
     ap.add_argument("--no-pipeline", action="store_true",
-                    help="synchronous rgc_run per step instead of two contexts in flight")
+                    help="synchronous rgc_run per step instead of contexts in flight")
     ap.add_argument("--streams", type=int, choices=(1, 2), default=2,
-                    help="pipelined steps: 2 (default) puts the two contexts on two streams, so "
-                         "step i+1 runs in step i's drain tail; 1 serialises them on one stream "
-                         "(the rocprof evidence command: per-launch durations that do not "
-                         "overlap)")
+                    help="pipelined steps: 2 (default) puts each context in flight (three) on a "
+                         "stream of its own, so step i+1 runs in step i's drain tail; 1 "
+                         "serialises two contexts on one stream (the rocprof evidence command: "
+                         "per-launch durations that do not overlap)")
     ap.add_argument("--by-config", default=None,
                     help="comma-separated by_config entries (BY_CONFIG names) also timed in this "
                          "run (default: every other BASELINE config at its bench size plus "

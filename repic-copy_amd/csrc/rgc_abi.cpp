@@ -207,8 +207,6 @@ struct rgc_ctx {
   size_t slots_off = 0;      // ... at this offset
   int pend_slot = 0;         // cursor slot of the submitted run
   int lazy_n_mg = -1;        // micrographs of the last lazy-stats run not yet fetched
-  hipStream_t copy_stream = nullptr;   // rgc_submit: stats copy off the launch stream
-  hipEvent_t ev_k = nullptr;           // rgc_submit: after the fused launch
   hipEvent_t ev_tail = nullptr;    // timing: recorded after each fused pass's stats copy   // fused cursor already cleared on the stream for next run
   std::vector<uint64_t> stamps;   // diagnostic build only
   // rgc_submit / rgc_wait: one run in flight per context
@@ -1204,22 +1202,21 @@ static int submit_fast(rgc_ctx* c, const rgc_batch_in* in) {
     if (!c->ev_tail) HIPCHK(hipEventCreate(&c->ev_tail));
     HIPCHK(hipEventRecord(c->ev_tail, s));
   }
-  // the stats copy runs on the context's copy stream, so the next launch on the main stream
-  // does not wait for it (the next run on THIS context is submitted after rgc_wait)
-  if (!c->copy_stream) HIPCHK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
-  if (!c->ev_k) HIPCHK(hipEventCreateWithFlags(&c->ev_k, hipEventDisableTiming));
+  // the stats copy on the launch stream: the next run on THIS context is submitted after
+  // rgc_wait, and other contexts launch on streams of their own (bench.py: one stream per
+  // context; two contexts on ONE stream see the copy between their launches).  A side copy
+  // stream per context cost 3-4 % with two or three contexts in flight (its hardware queue is
+  // shared with the other contexts' launch streams: profiles/r05w_ab_copy_on_stream.txt).
   if (!c->ev_sub) HIPCHK(hipEventCreateWithFlags(&c->ev_sub, hipEventDisableTiming));
-  HIPCHK(hipEventRecord(c->ev_k, s));
-  HIPCHK(hipStreamWaitEvent(c->copy_stream, c->ev_k, 0));
   if (flags & RGC_F_LAZY_STATS) {   // the run's totals only; rgc_fetch_stats copies the rest
     const size_t so = cur_off + (size_t)io.slot * CUR_BYTES;
     HIPCHK(hipMemcpyAsync(H<char>(c, H_MGOUT) + so, D<char>(c, D_MGOUT) + so, CUR_BYTES,
-                          hipMemcpyDeviceToHost, c->copy_stream));
+                          hipMemcpyDeviceToHost, s));
   } else {
     HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOUT), D<void>(c, D_MGOUT), cur_off + 2 * CUR_BYTES,
-                          hipMemcpyDeviceToHost, c->copy_stream));
+                          hipMemcpyDeviceToHost, s));
   }
-  HIPCHK(hipEventRecord(c->ev_sub, c->copy_stream));
+  HIPCHK(hipEventRecord(c->ev_sub, s));
   HIPCHK(hipGetLastError());
   return 1;
 }
@@ -1314,11 +1311,6 @@ void rgc_ctx_destroy(rgc_ctx* c) {
   for (auto e : c->events) (void)hipEventDestroy(e);
   if (c->ev_tail) (void)hipEventDestroy(c->ev_tail);
   if (c->ev_sub) (void)hipEventDestroy(c->ev_sub);
-  if (c->ev_k) (void)hipEventDestroy(c->ev_k);
-  if (c->copy_stream) {
-    (void)hipStreamSynchronize(c->copy_stream);
-    (void)hipStreamDestroy(c->copy_stream);
-  }
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1401,7 +1393,6 @@ int rgc_detach_host(rgc_ctx* c, void** block) {
   HIPCHK(hipSetDevice(c->device));
   TRY(rgc_fetch_stats(c));   // a lazy run's per-micrograph block lands in the detached buffer
   HIPCHK(hipStreamSynchronize(c->stream));
-  if (c->copy_stream) HIPCHK(hipStreamSynchronize(c->copy_stream));
   rgc_host_block* b = new rgc_host_block();
   for (auto& h : c->h) {
     if (h.p) b->bufs.push_back(h.p);
