@@ -217,6 +217,8 @@ struct rgc_ctx {
   rgc_batch_out pend_out{};
   hipEvent_t ev_sub = nullptr;   // after the submitted run's stats copy
   int qg_nslots = 0;             // HBM level-tree slots allocated (ensure_qg)
+  hipStream_t copy_stream = nullptr;   // rgc_submit: per-micrograph stats copy (non-lazy runs)
+  hipEvent_t ev_k = nullptr;           // rgc_submit: after the fused launch
   uint32_t tiles_epoch = 0;      // scan_epoch_count() when D_TILES was last zeroed
   // rgc_submit's general path (host syncs per clique level) runs here; rgc_wait joins it
   std::thread worker;
@@ -1202,21 +1204,28 @@ static int submit_fast(rgc_ctx* c, const rgc_batch_in* in) {
     if (!c->ev_tail) HIPCHK(hipEventCreate(&c->ev_tail));
     HIPCHK(hipEventRecord(c->ev_tail, s));
   }
-  // the stats copy on the launch stream: the next run on THIS context is submitted after
-  // rgc_wait, and other contexts launch on streams of their own (bench.py: one stream per
-  // context; two contexts on ONE stream see the copy between their launches).  A side copy
-  // stream per context cost 3-4 % with two or three contexts in flight (its hardware queue is
-  // shared with the other contexts' launch streams: profiles/r05w_ab_copy_on_stream.txt).
+  // The stats copy.  A lazy run's (its 128-B totals) on the launch stream: the next run on
+  // THIS context is submitted after rgc_wait, and other contexts launch on streams of their
+  // own (bench.py: one stream per context), whose hardware queues a side copy stream per
+  // context would share (3-4 % with two or three contexts in flight,
+  // profiles/r05w_ab_copy_on_stream.txt).  Every micrograph's stats (48 B each) on the
+  // context's side copy stream after an event: as a blit kernel on the launch stream that copy
+  // waits for CUs behind the other contexts' workgroups (C2: 0.39 -> 0.56 ms per step).
   if (!c->ev_sub) HIPCHK(hipEventCreateWithFlags(&c->ev_sub, hipEventDisableTiming));
   if (flags & RGC_F_LAZY_STATS) {   // the run's totals only; rgc_fetch_stats copies the rest
     const size_t so = cur_off + (size_t)io.slot * CUR_BYTES;
     HIPCHK(hipMemcpyAsync(H<char>(c, H_MGOUT) + so, D<char>(c, D_MGOUT) + so, CUR_BYTES,
                           hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(c->ev_sub, s));
   } else {
+    if (!c->copy_stream) HIPCHK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    if (!c->ev_k) HIPCHK(hipEventCreateWithFlags(&c->ev_k, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(c->ev_k, s));
+    HIPCHK(hipStreamWaitEvent(c->copy_stream, c->ev_k, 0));
     HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOUT), D<void>(c, D_MGOUT), cur_off + 2 * CUR_BYTES,
-                          hipMemcpyDeviceToHost, s));
+                          hipMemcpyDeviceToHost, c->copy_stream));
+    HIPCHK(hipEventRecord(c->ev_sub, c->copy_stream));
   }
-  HIPCHK(hipEventRecord(c->ev_sub, s));
   HIPCHK(hipGetLastError());
   return 1;
 }
@@ -1311,6 +1320,11 @@ void rgc_ctx_destroy(rgc_ctx* c) {
   for (auto e : c->events) (void)hipEventDestroy(e);
   if (c->ev_tail) (void)hipEventDestroy(c->ev_tail);
   if (c->ev_sub) (void)hipEventDestroy(c->ev_sub);
+  if (c->ev_k) (void)hipEventDestroy(c->ev_k);
+  if (c->copy_stream) {
+    (void)hipStreamSynchronize(c->copy_stream);
+    (void)hipStreamDestroy(c->copy_stream);
+  }
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1393,6 +1407,7 @@ int rgc_detach_host(rgc_ctx* c, void** block) {
   HIPCHK(hipSetDevice(c->device));
   TRY(rgc_fetch_stats(c));   // a lazy run's per-micrograph block lands in the detached buffer
   HIPCHK(hipStreamSynchronize(c->stream));
+  if (c->copy_stream) HIPCHK(hipStreamSynchronize(c->copy_stream));
   rgc_host_block* b = new rgc_host_block();
   for (auto& h : c->h) {
     if (h.p) b->bufs.push_back(h.p);
