@@ -39,7 +39,41 @@ DEFAULT_MG = {"C2": 10000, "C3": 4000, "C4": 12500, "C5": 64}
 # C5_256: the large-micrograph route at 256 micrographs per step (its per-micrograph kernels,
 # one workgroup per micrograph, fill 64 of 256 CUs at C5's 64 per step)
 BY_CONFIG = {"C2": ("C2", 10000), "C3": ("C3", 4000), "C4": ("C4", 12500), "C5": ("C5", 64),
-             "C4_100k": ("C4", 100000), "C5_256": ("C5", 256)}
+             "C4_100k": ("C4", 100000), "C5_256": ("C5", 256),
+             # strong scaling: ONE fixed 100k-micrograph C4 batch (the
+             # north-star batch) split over the ranks, 100k / N each; at N = 1 it is C4_100k
+             "C4_100k_fixed": ("C4", 100000)}
+FIXED_TOTAL = {"C4_100k_fixed"}   # entries whose micrograph count is the whole job's, not per GPU
+# file-to-file entries (the CLI on BOX text, one GPU, rank 0 of a 1-GPU run): C1 = the
+# reference's own EMPIAR-10017 example (12 micrographs, BASELINE configs[0]), C2_f2f = 10k
+# synthetic C2 micrographs written as BOX text first (not timed)
+F2F_ENTRIES = ("C1", "C2_f2f")
+# the reference's C1 rate (the survey's run of the reference itself, 1 core,
+# 34.75 s for the 12 micrographs; README.md:60 quotes "1-3 mins")
+REF_C1_RATE = 0.345
+# hardware queues per process on the MI355X boxes (GPU_MAX_HW_QUEUES); the bench's streams:
+# `depth` launch streams + torch's null stream, which also carries the non-lazy stats copies
+HW_QUEUES = 4
+
+
+def fixed_shard(total, world, rank):
+    """(start, count) of rank's contiguous share of a fixed batch of ``total`` micrographs:
+    sizes differ by at most one, the first ``total % world`` ranks take the extra one."""
+    base, extra = divmod(total, world)
+    start = rank * base + min(rank, extra)
+    return start, base + (1 if rank < extra else 0)
+
+
+def stream_plan(depth):
+    """Streams (hardware queues) one bench process uses: a launch stream per context in flight
+    plus the null stream (torch's default; the library copies non-lazy per-micrograph stats
+    on it, rgc_ctx_set_copy_stream(ctx, 0)), no other copy stream.  Must fit HW_QUEUES, or
+    streams share queues in creation order (round 5: the stats-copy variant ran 68 % slower
+    on the driver's box with 7 streams)."""
+    plan = {"launch_streams": depth, "null_stream": 1, "copy_streams": 0}
+    plan["total"] = plan["launch_streams"] + plan["null_stream"] + plan["copy_streams"]
+    assert plan["total"] <= HW_QUEUES, plan
+    return plan
 
 
 def fused_compulsory_bytes(N, C, k, V, n_mg):
@@ -74,10 +108,12 @@ def pipeline_bytes(N, E, C, k):
     return 28 * N + 32 * E + C * (20 * k + 12)
 
 
-def pmc_record(config):
+def pmc_record(entry):
     """The newest profiles/*_traffic.json written by tools/pmc_traffic.py for THIS library
-    build (sha256 must match) on THIS workload (config; files without one were C2 runs), as
-    (record, file name), else (None, None)."""
+    build (sha256 must match) on THIS entry (its by_config name, which fixes the batch size:
+    files without an "entry" key were taken at the config's bench size, so they stand for the
+    entry named like the config, and files without a "config" were C2 runs), as (record, file
+    name), else (None, None)."""
     import glob
     import hashlib
     from repic_amd import _lib
@@ -87,7 +123,7 @@ def pmc_record(config):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if d.get("lib_sha256") == sha and d.get("config", "C2") == config:
+        if d.get("lib_sha256") == sha and d.get("entry", d.get("config", "C2")) == entry:
             return d, os.path.basename(f)
     return None, None
 
@@ -371,10 +407,12 @@ def pipelined_steps(ctxs, submit, n, timing, ktimes=None):
 
 
 def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=False,
-            lazy_stats=True, streams=1, depth=None):
+            lazy_stats=True, streams=1, depth=None, entry=None, fixed_total=None):
     """Time ``steps`` steps of the hot path over one synthetic batch of ``config`` (n_mg
-    micrographs per rank, inputs resident in HBM): barrier + synchronize on both sides, max
-    over ranks.  Returns (report dict, cfg, this rank's micrographs)."""
+    micrographs per rank, inputs resident in HBM; with ``fixed_total``, this rank's share of
+    one batch of that many micrographs): barrier + synchronize on both sides, max over ranks.
+    ``entry`` names the workload for its PMC record (default: the config).  Returns (report
+    dict, cfg, this rank's micrographs)."""
     import torch
 
     from repic_amd import _lib, synth
@@ -382,15 +420,18 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
 
     dist, world, rank, dev, cdev = env.dist, env.world, env.rank, env.dev, env.cdev
     depth = depth or PIPE_DEPTH.get(config, PIPE_DEPTH_DEFAULT)
+    entry = entry or config
     cfg = synth.SynthConfig(**synth.CONFIGS[config], seed=args.seed)
     t_gen = time.time()
     # this rank's shard of one big batch (identical to packing synth.batch's list; large
     # batches are generated by a process pool)
+    start = rank * n_mg
+    if fixed_total is not None:   # strong scaling: a share of one fixed batch
+        start, n_mg = fixed_shard(fixed_total, world, rank)
     procs = min(16, len(os.sched_getaffinity(0))) if n_mg * cfg.n_true * cfg.k >= 2_000_000 else 1
-    batch = Batch.from_counts(cfg.k, cfg.box, *synth.packed(cfg, n_mg, start=rank * n_mg,
-                                                             procs=procs))
+    batch = Batch.from_counts(cfg.k, cfg.box, *synth.packed(cfg, n_mg, start=start, procs=procs))
     # the first micrographs as per-picker arrays, for the CPU baseline's sample
-    mgs = synth.batch(cfg, min(n_mg, 64 if config != "C3" else 8), start=rank * n_mg)
+    mgs = synth.batch(cfg, min(n_mg, 64 if config != "C3" else 8), start=start)
     t_gen = time.time() - t_gen
     # the one exchange of the sharded path: global box-id offsets
     if dist is not None:
@@ -412,7 +453,9 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
     # one explicit stream for every context (torch's default stream handle is 0, with which
     # each context would create its own stream, and two in-flight steps would run their
     # kernels concurrently: more throughput, but per-launch kernel times that overlap)
-    # (the process's streams, created once: every measure() runs on the same ones)
+    # (the process's streams, created once: every measure() runs on the same ones; with the
+    # null stream they fit the hardware queues, stream_plan)
+    stream_plan(depth)
     if env.streams is None:
         env.streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
     while len(env.streams) < depth:   # (experiments: tools/streams_ab.py --depth)
@@ -432,6 +475,8 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
                         for j in range(1, depth)]
     else:
         ctxs = [ctx, _lib.Context(env.local, stream)] if pipeline else [ctx]
+    for c in ctxs:   # non-lazy stats copies on the null stream: no extra hardware queue
+        c.set_copy_stream(0)
 
     def step(timing=False):
         if host_io:
@@ -524,7 +569,7 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
         dom_bytes = pipe
         dom_ms = dev_ms
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    rec, traffic_src = pmc_record(config)
+    rec, traffic_src = pmc_record(entry)
     kind = "k_fused" if dom == "k_fused" else "route"
     dv_kernel = "k_fused" if kind == "k_fused" else max(avg, key=avg.get)
     traffic, hbm_frac, limiter = roofline_evidence(rec, kind, dom_bytes, dom_ms, dv_kernel)
@@ -532,12 +577,16 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
         "value": value, "unit": "micrographs/s", "n_gpus": world, "steps": steps,
         "warmup": warmup, "ms_per_step": elapsed / steps * 1e3,
         "config": {"workload": f"{config}: {synth.CONFIGS[config]}",
-                   "micrographs_per_gpu": n_mg, "k": cfg.k, "box_size": cfg.box,
+                   "micrographs_per_gpu": n_mg if fixed_total is None else fixed_total / world,
+                   "micrographs_per_step": tot_mg,
+                   "scaling": "weak" if fixed_total is None else "strong",
+                   "k": cfg.k, "box_size": cfg.box,
                    "boxes_per_gpu": N, "edges_per_gpu": E, "cliques_per_gpu": C,
                    "parallelism": f"dp{world} (micrograph shards)",
                    "io": "host buffers over PCIe (--host-io)" if host_io else "HBM-resident",
                    "steps_in_flight": len(ctxs) if pipeline else 1,
-                   "streams": len(ctxs) if overlap else 1},
+                   "streams": len(ctxs) if overlap else 1,
+                   "stream_plan": stream_plan(depth)},
         "edges_per_sec": tot_e * steps / elapsed,
         "totals": {"micrographs": tot_mg, "edges": tot_e, "cliques": tot_c},
         "roofline": {"bound": derived_bound(rec, kind, dom_bytes, dom_ms, dv_kernel),
@@ -577,6 +626,8 @@ def by_config_entry(rep):
             "kernel_ms": r["kernel_ms_per_step"], "kernel": r["kernel"],
             "steps": rep["steps"], "warmup": rep["warmup"],
             "micrographs_per_gpu": rep["config"]["micrographs_per_gpu"],
+            "micrographs_per_step": rep["config"]["micrographs_per_step"],
+            "scaling": rep["config"]["scaling"],
             "edges_per_sec": rep["edges_per_sec"], "totals": rep["totals"],
             "roofline": {"frac": r["frac"], "achieved": r["achieved"], "bound": r["bound"],
                          "traffic": r["traffic"], "traffic_source": r["traffic_source"],
@@ -644,7 +695,8 @@ def main():
     # C4 at the 100k / 8-GPU shard of 12.5k micrographs per GPU, C4_100k the whole north-star
     # batch on this GPU), each with a 1-core CPU baseline sample on rank 0
     if args.by_config is None:
-        extra = [] if args.n_mg else [c for c in ("C2", "C3", "C4", "C5", "C4_100k", "C5_256")
+        extra = [] if args.n_mg else [c for c in ("C2", "C3", "C4", "C5", "C4_100k", "C5_256",
+                                                  "C4_100k_fixed", "C1", "C2_f2f")
                                       if c != args.config]
     elif args.by_config.lower() == "none":
         extra = []
@@ -655,9 +707,22 @@ def main():
         byc = {args.config: by_config_entry(rep)}
         cpu_of = {}
         for name in extra:
+            if name in F2F_ENTRIES:
+                # file to file: the CLI on one GPU (rank 0 of a 1-GPU run only)
+                if world == 1:
+                    byc[name] = f2f_entry(name, cpu=cpu_rank0 and not args.no_cpu_baseline
+                                          and args.by_config_cpu_budget > 0,
+                                          cpu_budget=args.by_config_cpu_budget)
+                continue
             config, n_c = BY_CONFIG[name]
+            if name in FIXED_TOTAL and world == 1 and "C4_100k" in byc:
+                # one GPU: the fixed 100k batch IS C4_100k's (same micrographs, same steps)
+                byc[name] = dict(byc["C4_100k"], scaling="strong", same_run_as="C4_100k")
+                continue
             r_c, cfg_c, mgs_c = measure(args, env, config, n_c, args.steps, args.warmup,
-                                        no_pipeline=args.no_pipeline, streams=args.streams)
+                                        no_pipeline=args.no_pipeline, streams=args.streams,
+                                        entry=name,
+                                        fixed_total=n_c if name in FIXED_TOTAL else None)
             byc[name] = by_config_entry(r_c)
             if cpu_rank0 and args.by_config_cpu_budget > 0 and not args.no_cpu_baseline:
                 if config not in cpu_of:
@@ -685,6 +750,113 @@ def main():
         print(json.dumps(out), flush=True)
     if env.dist is not None:
         env.dist.destroy_process_group()
+
+
+def _cli_run(in_dir, out_dir, box, threads=None):
+    """One run of the drop-in CLI (repic_amd.commands.get_cliques.main), stdout silenced;
+    returns (wall seconds, its LAST_RUN phase record)."""
+    import repic_amd.commands.get_cliques as gc
+    p = argparse.ArgumentParser()
+    gc.add_arguments(p)
+    argv = [in_dir, out_dir, str(box)] + (["--threads", str(threads)] if threads else [])
+    cli = p.parse_args(argv)
+    so = sys.stdout
+    with open(os.devnull, "w") as dn:
+        sys.stdout = dn
+        try:
+            t0 = time.perf_counter()
+            gc.main(cli)
+            wall = time.perf_counter() - t0
+        finally:
+            sys.stdout = so
+    return wall, dict(gc.LAST_RUN)
+
+
+def _c1_cpu_sample(in_dir, budget_s):
+    """The oracle's faithful per-micrograph path (oracle/cpu_ref.py, the reference's
+    get_jaccard loop structure) on the 10017 micrographs, parsed (untimed) by the product's
+    ingest plan, until ``budget_s`` has elapsed: (micrographs, seconds) on 1 core."""
+    from oracle import cpu_ref
+    from repic_amd import ingest
+    methods = ingest.list_methods(in_dir)
+    mgs, _, _ = ingest.plan(in_dir, methods, ingest.DirIndex(in_dir, methods))
+    t0 = time.perf_counter()
+    n = 0
+    for mg in mgs:
+        if mg.status != "ok":
+            continue
+        nid, coords = mg.id_base, []
+        for pf in mg.coords:
+            coords.append([(float(a), float(b), float(c), nid + i)
+                           for i, (a, b, c) in enumerate(zip(pf.x, pf.y, pf.s))])
+            nid += pf.n
+        cpu_ref.micrograph(coords, 180, methods, faithful=True)
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    return n, time.perf_counter() - t0
+
+
+def f2f_entry(name, cpu=True, cpu_budget=6.0):
+    """File-to-file rate of the drop-in CLI (BOX text in, the five files per micrograph out),
+    never the headline: C1 = the reference's EMPIAR-10017 example (tests/golden/inputs_10017,
+    12 micrographs; a warm-up run, then the median of 5 timed runs, each into a fresh output
+    directory) beside the reference's own rate on it; C2_f2f = 10k C2 micrographs written as
+    BOX text to /tmp first (not timed), then one timed CLI run (a first run: the writes of 50k
+    fresh files depend on the file system's state)."""
+    import shutil
+    import tempfile
+    work = tempfile.mkdtemp(prefix="rgc_bench_f2f_", dir="/tmp")
+    try:
+        if name == "C1":
+            in_dir = os.path.join(ROOT, "tests", "golden", "inputs_10017")
+            n_mg, box = 12, 180
+            _cli_run(in_dir, os.path.join(work, "warm"), box)
+            walls, last = [], None
+            for i in range(5):
+                w, last = _cli_run(in_dir, os.path.join(work, f"out{i}"), box)
+                walls.append(w)
+            wall = float(np.median(walls))
+            out = {"value": n_mg / wall, "unit": "micrographs/s (file to file)",
+                   "micrographs": n_mg, "wall_s": wall, "wall_s_runs": walls,
+                   "workload": "EMPIAR-10017 example (BASELINE configs[0]): crYOLO / deepPicker "
+                               "/ topaz BOX, box 180, the reference's own input files",
+                   "phases_s": {k_: round(v, 4) for k_, v in last.items() if k_.endswith("_s")},
+                   "cliques": last.get("cliques"),
+                   "reference_cpu": {"value": REF_C1_RATE, "unit": "micrographs/s",
+                                     "cores": 1, "kind": "reference",
+                                     "source": "BASELINE.md §2: the reference's get_cliques run "
+                                               "on these files, 1 core (34.75 s)"}}
+            out["vs_reference_cpu"] = out["value"] / REF_C1_RATE
+            if cpu:
+                n, dt = _c1_cpu_sample(in_dir, cpu_budget)
+                out["cpu_baseline"] = {"value": n / dt, "unit": "micrographs/s", "cores": 1,
+                                       "kind": "port", "cpu_model": _cpu_model(),
+                                       "sample": f"{n} of the 12 micrographs, oracle faithful "
+                                                 f"path, 1 process, {dt:.1f} s"}
+            return out
+        from repic_amd import synth
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from file_bench import _write_inputs as write_inputs
+        cfg = synth.SynthConfig(**synth.CONFIGS["C2"], seed=0)
+        n_mg = 10000
+        threads = min(16, len(os.sched_getaffinity(0)))
+        in_dir = os.path.join(work, "in")
+        t0 = time.perf_counter()
+        write_inputs(in_dir, cfg, n_mg, threads)
+        gen = time.perf_counter() - t0
+        warm = os.path.join(work, "warm")
+        synth.write_box_dirs(warm, cfg, 2)
+        _cli_run(warm, os.path.join(work, "warm_out"), cfg.box)
+        wall, last = _cli_run(in_dir, os.path.join(work, "out"), cfg.box, threads)
+        return {"value": n_mg / wall, "unit": "micrographs/s (file to file)",
+                "micrographs": n_mg, "wall_s": wall, "gen_s": gen, "threads": threads,
+                "workload": "C2 (10k synthetic micrographs x 3 pickers as BOX text in /tmp, "
+                            "box 180), first run",
+                "phases_s": {k_: round(v, 4) for k_, v in last.items() if k_.endswith("_s")},
+                "cliques": last.get("cliques"), "edges": last.get("edges")}
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
 
 
 def glob_pairing_term(n_mg, k, sample=20000):

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define RGC_ABI_VERSION 8
+#define RGC_ABI_VERSION 9
 
 /* flags for rgc_batch_in.flags */
 #define RGC_F_GET_CC         1u  /* --get_cc   (get_cliques.py:151-156) */
@@ -120,6 +120,11 @@ int rgc_device_count(int* n);
 
 int rgc_ctx_create(int device, void* hip_stream, rgc_ctx** out);
 void rgc_ctx_destroy(rgc_ctx* ctx);
+/* ABI 9: the stream of a submitted non-lazy run's per-micrograph stats copy (hip_stream may be
+ * 0: the device's null stream).  Without a call every context of the process shares one copy
+ * stream per device, so N contexts on N launch streams take N + 1 hardware queues, not 2 N
+ * (GPU_MAX_HW_QUEUES is 4 on the MI355X boxes). */
+int rgc_ctx_set_copy_stream(rgc_ctx* ctx, void* hip_stream);
 int rgc_run(rgc_ctx* ctx, const rgc_batch_in* in, rgc_batch_out* out);
 /* Asynchronous rgc_run (ABI 3), one run in flight per context: rgc_submit enqueues the batch
  * on the context's stream and returns; rgc_wait blocks until it is done and fills *out exactly
@@ -177,7 +182,10 @@ int rgc_score_pairs(rgc_ctx* ctx, const rgc_score_in* in, int64_t* counts);
  * exactly, for a batch of micrographs at once (rows are global box ids: micrographs never
  * share a row).  A is given in CSC form.  x[c] = 1 for the chosen columns (cliques);
  * exact[c] is the status of column c's conflict component:
- *   RGC_ILP_OPTIMAL  (1) proven optimal by the branch and bound;
+ *   RGC_ILP_OPTIMAL  (1) proven optimal: by the branch and bound, or (ABI 9) for a component
+ *                        the search could not finish, by the exact search of the columns its
+ *                        Lagrangian reduced costs leave (reduced-cost fixing: every packing
+ *                        that uses another column is worth less than the certified one);
  *   RGC_ILP_GAP_OK   (2) not searched to the end (more than 4096 cliques, or node_limit hit),
  *                        but a Lagrangian dual bound certifies x within a relative gap of 1e-4,
  *                        the default MIPGap at which Gurobi reports a model optimal;
@@ -189,24 +197,28 @@ int rgc_score_pairs(rgc_ctx* ctx, const rgc_score_in* in, int64_t* counts);
 #define RGC_ILP_OPTIMAL 1
 #define RGC_ILP_GAP_OK 2
 #define RGC_ILP_HEURISTIC 3
+#define RGC_ILP_DEFAULT_NODES (1 << 14)
 typedef struct rgc_ilp_in {
   int64_t n_cols;          /* cliques */
   int64_t n_rows;          /* boxes */
   const int64_t* col_ptr;  /* [n_cols + 1] column c's rows: row_idx[col_ptr[c], col_ptr[c+1]) */
   const int32_t* row_idx;  /* [nnz] global row ids */
   const double* w;         /* [n_cols] objective */
-  int64_t node_limit;      /* branch-and-bound nodes per component (0: 2^22); components of more
-                              than 1024 cliques get node_limit * 1024 / n (work-scaled) */
+  int64_t node_limit;      /* branch-and-bound nodes per component (0: RGC_ILP_DEFAULT_NODES);
+                              components of more than 1024 cliques get node_limit * 16 / W,
+                              W = 64-clique words (work-scaled); each reduced-cost-fixing pass
+                              (up to 2 below the first) searches with 4x the nodes of the one
+                              above.  The node budgets are the only limit of the search, so
+                              the result is deterministic */
   uint32_t flags;          /* RGC_F_TIMING */
   double* gap;             /* optional (NULL: not returned), ABI 6: [n_cols] dual bound minus
                             * packing value of column c's component, at the component's first
                             * column (0 elsewhere and for proven-optimal components), so a
                             * caller can certify a whole micrograph the way Gurobi's MIPGap
                             * does (sum of gaps <= 1e-4 x its objective) */
-  double time_limit_s;     /* ABI 8: seconds the branch-and-bound search of the 65..4096-clique
-                            * components may take (<= 0: no limit); components it does not
-                            * reach are packed and certified like the larger ones, components it
-                            * stops in keep their incumbent (status by the certified gap) */
+  double time_limit_s;     /* ABI 8, ignored since ABI 9: the search ran under a wall-clock budget,
+                            * which made x depend on the device's speed and load; it is bounded
+                            * by node budgets only now (kept for the struct layout) */
 } rgc_ilp_in;
 int rgc_ilp_solve(rgc_ctx* ctx, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact);
 

@@ -74,6 +74,7 @@ enum DevBufId {
   D_IL_RPTR, D_IL_RCOLS, D_IL_CID, D_IL_CN, D_IL_COFF, D_IL_CCUR, D_IL_MEM, D_IL_LOC, D_IL_SCR,
   D_IL_BIG, D_IL_NBIG, D_IL_WSCR, D_IL_X, D_IL_EX, D_IL_RLOC, D_IL_CERT, D_IL_KEY, D_IL_ST,
   D_IL_RMAX, D_IL_OWN, D_IL_LAM, D_IL_GRAD, D_IL_CS, D_IL_CNT, D_IL_GAP, D_IL_STSAVE,
+  D_IL_FS, D_IL_FSCNT, D_IL_FSKEEP,
   D_COUNT
 };
 enum HostBufId {
@@ -187,6 +188,18 @@ static const FusedPlan& cached_plan(int k, int pass, int nmax) {
 
 }  // namespace
 
+// one side copy stream per device for the whole process (created on first use, kept for the
+// process's lifetime)
+static int shared_copy_stream(int device, hipStream_t* out) {
+  static std::mutex mu;
+  static std::vector<hipStream_t> streams;
+  std::lock_guard<std::mutex> lk(mu);
+  if ((int)streams.size() <= device) streams.resize(device + 1, nullptr);
+  if (!streams[device]) HIPCHK(hipStreamCreateWithFlags(&streams[device], hipStreamNonBlocking));
+  *out = streams[device];
+  return 0;
+}
+
 struct rgc_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -217,9 +230,13 @@ struct rgc_ctx {
   rgc_batch_out pend_out{};
   hipEvent_t ev_sub = nullptr;   // after the submitted run's stats copy
   int qg_nslots = 0;             // HBM level-tree slots allocated (ensure_qg)
-  hipStream_t copy_stream = nullptr;   // rgc_submit: per-micrograph stats copy (non-lazy runs)
+  // rgc_submit: stream of the per-micrograph stats copy (non-lazy runs).  Unless the caller
+  // names one (rgc_ctx_set_copy_stream, ABI 9), the process-wide copy stream of the device,
+  // shared by every context: streams beyond GPU_MAX_HW_QUEUES (4) share hardware queues
+  bool copy_set = false;
+  hipStream_t copy_stream = nullptr;
   hipEvent_t ev_k = nullptr;           // rgc_submit: after the fused launch
-  uint32_t tiles_epoch = 0;      // scan_epoch_count() when D_TILES was last zeroed
+  uint64_t tiles_epoch = 0;      // scan_epoch_count() when D_TILES was last zeroed
   // rgc_submit's general path (host syncs per clique level) runs here; rgc_wait joins it
   std::thread worker;
   std::string pend_err;          // the worker's error message (g_err is per thread)
@@ -493,6 +510,7 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
   const int64_t E = H<int64_t>(c, H_TOTAL)[0];
+  if (E < 0) return fail("edge scan: look-back guard exhausted (stale tile buffer)");
   *E_out = E;
   TRY(ensure_dev(c, D_EDST, E * 4));
   TRY(ensure_dev(c, D_ADJG, E * 8));
@@ -563,6 +581,7 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
     HIPCHK(hipStreamSynchronize(s));
     const int64_t nn = h_tot[2];
     C2 = h_tot[1];
+    if (nn < 0 || C2 < 0) return fail("clique scan: look-back guard exhausted (stale tile buffer)");
     if (leaf) {
       C1 = nn;
       break;
@@ -1218,7 +1237,10 @@ static int submit_fast(rgc_ctx* c, const rgc_batch_in* in) {
                           hipMemcpyDeviceToHost, s));
     HIPCHK(hipEventRecord(c->ev_sub, s));
   } else {
-    if (!c->copy_stream) HIPCHK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    if (!c->copy_set) {
+      TRY(shared_copy_stream(c->device, &c->copy_stream));
+      c->copy_set = true;
+    }
     if (!c->ev_k) HIPCHK(hipEventCreateWithFlags(&c->ev_k, hipEventDisableTiming));
     HIPCHK(hipEventRecord(c->ev_k, s));
     HIPCHK(hipStreamWaitEvent(c->copy_stream, c->ev_k, 0));
@@ -1289,6 +1311,15 @@ int rgc_device_count(int* n) {
   return 0;
 }
 
+int rgc_ctx_set_copy_stream(rgc_ctx* c, void* hip_stream) {
+  if (!c) return fail("null context");
+  if (c->pend) return fail("rgc_ctx_set_copy_stream: a submitted run awaits rgc_wait");
+  if (c->copy_set) HIPCHK(hipStreamSynchronize(c->copy_stream));
+  c->copy_stream = reinterpret_cast<hipStream_t>(hip_stream);
+  c->copy_set = true;
+  return 0;
+}
+
 int rgc_ctx_create(int device, void* hip_stream, rgc_ctx** out) {
   *out = nullptr;
   HIPCHK(hipSetDevice(device));
@@ -1321,10 +1352,7 @@ void rgc_ctx_destroy(rgc_ctx* c) {
   if (c->ev_tail) (void)hipEventDestroy(c->ev_tail);
   if (c->ev_sub) (void)hipEventDestroy(c->ev_sub);
   if (c->ev_k) (void)hipEventDestroy(c->ev_k);
-  if (c->copy_stream) {
-    (void)hipStreamSynchronize(c->copy_stream);
-    (void)hipStreamDestroy(c->copy_stream);
-  }
+  if (c->copy_set) (void)hipStreamSynchronize(c->copy_stream);   // (not owned: never destroyed)
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1407,7 +1435,7 @@ int rgc_detach_host(rgc_ctx* c, void** block) {
   HIPCHK(hipSetDevice(c->device));
   TRY(rgc_fetch_stats(c));   // a lazy run's per-micrograph block lands in the detached buffer
   HIPCHK(hipStreamSynchronize(c->stream));
-  if (c->copy_stream) HIPCHK(hipStreamSynchronize(c->copy_stream));
+  if (c->copy_set) HIPCHK(hipStreamSynchronize(c->copy_stream));
   rgc_host_block* b = new rgc_host_block();
   for (auto& h : c->h) {
     if (h.p) b->bufs.push_back(h.p);
@@ -1537,16 +1565,20 @@ int rgc_score_pairs(rgc_ctx* c, const rgc_score_in* in, int64_t* counts) {
   return 0;
 }
 
-int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) {
-  if (!c || !in || !x || !exact) return fail("null argument");
-  if (c->pend) return fail("rgc_ilp_solve: a submitted run awaits rgc_wait on this context");
-  HIPCHK(hipSetDevice(c->device));
+// One pass of the device solver over a CSC batch (rgc_ilp_solve runs it once, then once more
+// on the reduced-cost-fixed columns of the components it left unproven): x, statuses and the
+// per-component gaps (gap_out, at one column of each component) on the host.  With fix set,
+// the kept columns of the certified components come back too (rgc_ilp.hip k_fs_*).
+struct IlpFix {
+  std::vector<uint8_t> keep;    // [n_cols] kept by reduced-cost fixing
+  std::vector<int32_t> comp;    // [n_cols] component of each column
+  std::vector<uint32_t> cnt;    // [n_comp] kept columns per component
+  std::vector<uint8_t> cert;    // [n_comp] 0: proven by the search, else certified
+};
+
+static int ilp_core(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact,
+                    double* gap_out, IlpFix* fix) {
   const int64_t nc = in->n_cols, nr = in->n_rows;
-  if (nc < 0 || nc >= INT32_MAX || nr < 0 || nr >= INT32_MAX) return fail("n_cols / n_rows out of range");
-  c->times.clear();
-  c->time_names.clear();
-  c->n_ev = 0;
-  c->timing = (in->flags & RGC_F_TIMING) != 0;
   if (nc == 0) return 0;
   const int64_t nnz = in->col_ptr[nc];
   if (in->col_ptr[0] != 0 || nnz < 0) return fail("col_ptr must start at 0");
@@ -1591,7 +1623,7 @@ int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) 
   A.n_cols = nc;
   A.n_rows = nr;
   A.kmax = kmax;
-  A.node_limit = in->node_limit > 0 ? in->node_limit : (int64_t)1 << 22;
+  A.node_limit = in->node_limit > 0 ? in->node_limit : (int64_t)RGC_ILP_DEFAULT_NODES;
   A.col_ptr = D<int64_t>(c, D_IL_CPTR);
   A.row_idx = D<int32_t>(c, D_IL_ROW);
   A.w = D<double>(c, D_IL_W);
@@ -1620,6 +1652,7 @@ int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) 
               D<int64_t>(c, D_TOTAL) + 1);
   HIPCHK(hipStreamSynchronize(s));
   const int64_t ncomp = H<int64_t>(c, H_TOTAL)[0];
+  if (ncomp < 0) return fail("component scan: look-back guard exhausted (stale tile buffer)");
   TRY(ensure_dev(c, D_IL_CN, (ncomp + 1) * 4));
   TRY(ensure_dev(c, D_IL_COFF, (ncomp + 1) * 8));
   TRY(ensure_dev(c, D_IL_CCUR, (ncomp + 1) * 4));
@@ -1660,14 +1693,10 @@ int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) 
   A.cs = D<double>(c, D_IL_CS);
   A.count = D<unsigned int>(c, D_IL_CNT);
   A.st_save = D<uint8_t>(c, D_IL_STSAVE);
-  // the wave search's time budget (ABI 8 rgc_ilp_in.time_limit_s; <= 0: none)
-  A.wave_budget = in->time_limit_s > 0.0 ? (uint64_t)(in->time_limit_s * 1e8) : 0;
-  A.gap = nullptr;
-  if (in->gap) {   // (ABI 6) per-component gaps: zero for proven components
-    TRY(ensure_dev(c, D_IL_GAP, nc * 8));
-    A.gap = D<double>(c, D_IL_GAP);
-    HIPCHK(hipMemsetAsync(A.gap, 0, nc * 8, s));
-  }
+  // per-component gaps: zero for proven components
+  TRY(ensure_dev(c, D_IL_GAP, nc * 8));
+  A.gap = D<double>(c, D_IL_GAP);
+  HIPCHK(hipMemsetAsync(A.gap, 0, nc * 8, s));
   // rounds until a pass changes nothing (each round settles at least the heaviest undecided
   // clique / makes at least one improving swap, so both terminate); counters read every 4
   auto rounds = [&](int phase, int cap) -> int {
@@ -1741,14 +1770,164 @@ int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) 
     TRY(repack());
     for (int it = 0; it < 2000; ++it) rgc::launch_ilp_cert(s, 4, A);
     rgc::launch_ilp_cert(s, 5, A);
+    if (fix) {   // reduced-cost fixing of the certified components (the second pass's input)
+      TRY(ensure_dev(c, D_IL_FS, (ncomp + 1) * 16));
+      TRY(ensure_dev(c, D_IL_FSCNT, (ncomp + 1) * 4));
+      TRY(ensure_dev(c, D_IL_FSKEEP, nc));
+      A.fs = D<double>(c, D_IL_FS);
+      A.fs_cnt = D<unsigned int>(c, D_IL_FSCNT);
+      A.fs_keep = D<uint8_t>(c, D_IL_FSKEEP);
+      rgc::launch_ilp_cert(s, 10, A);
+      fix->keep.resize(nc);
+      fix->comp.resize(nc);
+      fix->cnt.resize(ncomp);
+      fix->cert.resize(ncomp);
+      HIPCHK(hipMemcpyAsync(fix->keep.data(), A.fs_keep, nc, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(fix->comp.data(), A.loc, nc * 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(fix->cnt.data(), A.fs_cnt, ncomp * 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(fix->cert.data(), A.cert, ncomp, hipMemcpyDeviceToHost, s));
+    }
   }
   TRY(mark(c, "d2h_x"));
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(x, A.x, nc, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(exact, A.exact, nc, hipMemcpyDeviceToHost, s));
-  if (A.gap) HIPCHK(hipMemcpyAsync(in->gap, A.gap, nc * 8, hipMemcpyDeviceToHost, s));
-  TRY(mark(c, "end"));
+  HIPCHK(hipMemcpyAsync(gap_out, A.gap, nc * 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  return 0;
+}
+
+// The device solver, then (depth < ILP_FIX_DEPTH) reduced-cost fixing of the components it
+// left unproven, solved by the same function one level down.
+constexpr int ILP_FIX_DEPTH = 3;
+
+static int ilp_solve_rec(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact,
+                         double* gap, int depth) {
+  const int64_t nc = in->n_cols, nr = in->n_rows;
+  if (nc == 0) return 0;
+  IlpFix fix;
+  TRY(ilp_core(c, in, x, exact, gap, depth + 1 < ILP_FIX_DEPTH ? &fix : nullptr));
+  // Next pass: the certified components whose reduced-cost-fixed column set is small enough
+  // for the exact search (and smaller than the component), solved as one batch.  A packing of
+  // component j that uses a fixed column is worth less than its packing P_j, so its optimum is
+  // max(P_j, optimum over the kept columns): proven when the second pass proves its part.
+  if (!fix.cnt.empty()) {
+    const int64_t ncomp = (int64_t)fix.cnt.size();
+    std::vector<int32_t> size(ncomp, 0);
+    std::vector<double> pval(ncomp, 0.0), gap1(ncomp, 0.0);
+    for (int64_t j = 0; j < nc; ++j) {
+      const int32_t q = fix.comp[j];
+      ++size[q];
+      if (x[j]) pval[q] += in->w[j];
+      gap1[q] += gap[j];
+    }
+    std::vector<uint8_t> elig(ncomp, 0);
+    int64_t sub_nc = 0, sub_nnz = 0;
+    for (int64_t q = 0; q < ncomp; ++q)
+      elig[q] = fix.cert[q] != 0 && gap1[q] > 0.0 && fix.cnt[q] > 0 &&
+                (int)fix.cnt[q] <= rgc::ilp_big_max() && (int32_t)fix.cnt[q] < size[q];
+    std::vector<int64_t> sub_ptr(1, 0);
+    std::vector<int32_t> sub_row;
+    std::vector<double> sub_w;
+    std::vector<int64_t> sub_col;   // original column of each sub column
+    for (int64_t j = 0; j < nc; ++j) {
+      if (!elig[fix.comp[j]] || !fix.keep[j]) continue;
+      for (int64_t e = in->col_ptr[j]; e < in->col_ptr[j + 1]; ++e) sub_row.push_back(in->row_idx[e]);
+      sub_nnz += in->col_ptr[j + 1] - in->col_ptr[j];
+      sub_ptr.push_back(sub_nnz);
+      sub_w.push_back(in->w[j]);
+      sub_col.push_back(j);
+      ++sub_nc;
+    }
+    if (sub_nc > 0) {
+      TRY(mark(c, "k_ilp_fixsearch"));
+      rgc_ilp_in sub{};
+      sub.n_cols = sub_nc;
+      sub.n_rows = nr;
+      sub.col_ptr = sub_ptr.data();
+      sub.row_idx = sub_row.data();
+      sub.w = sub_w.data();
+      // (4x the nodes one level down: its components are the few hard ones, restricted)
+      sub.node_limit = 4 * (in->node_limit > 0 ? in->node_limit : (int64_t)RGC_ILP_DEFAULT_NODES);
+      std::vector<uint8_t> sx(sub_nc), sex(sub_nc);
+      std::vector<double> sgap(sub_nc);
+      // (with RGC_F_TIMING the second pass's sections follow "k_ilp_fixsearch" in the list)
+      TRY(ilp_solve_rec(c, &sub, sx.data(), sex.data(), sgap.data(), depth + 1));
+      std::vector<double> rval(ncomp, 0.0), rgap(ncomp, 0.0);
+      std::vector<uint8_t> ropt(ncomp, 1);
+      for (int64_t i = 0; i < sub_nc; ++i) {
+        const int32_t q = fix.comp[sub_col[i]];
+        if (sx[i]) rval[q] += sub_w[i];
+        rgap[q] += sgap[i];
+        if (sex[i] != RGC_ILP_OPTIMAL) ropt[q] = 0;
+      }
+      // per eligible component: bound min(L, max(P, R + sub gap)); the better packing
+      std::vector<uint8_t> take(ncomp, 0), st(ncomp, 0);
+      std::vector<double> g(ncomp, 0.0);
+      for (int64_t q = 0; q < ncomp; ++q) {
+        if (!elig[q]) continue;
+        const double P = pval[q], L = P + gap1[q], R = rval[q];
+        const double ub = std::min(L, std::max(P, R + (ropt[q] ? 0.0 : rgap[q])));
+        take[q] = R > P;
+        const double v = take[q] ? R : P;
+        g[q] = std::max(0.0, ub - v);
+        st[q] = g[q] <= 0.0 ? RGC_ILP_OPTIMAL : g[q] <= 1e-4 * std::fabs(v) ? RGC_ILP_GAP_OK : 0;
+      }
+      if (std::getenv("RGC_ILP_DEBUG")) {
+        int64_t nel = 0, nopt = 0, nok = 0, ntake = 0, nflag = 0, nbig = 0, cmax = 0;
+        for (int64_t q = 0; q < ncomp; ++q) {
+          nflag += fix.cert[q] != 0;
+          if (fix.cert[q] && gap1[q] > 0.0) {
+            nbig += (int)fix.cnt[q] > rgc::ilp_big_max();
+            cmax = std::max<int64_t>(cmax, fix.cnt[q]);
+          }
+          if (!elig[q]) continue;
+          ++nel;
+          nopt += st[q] == RGC_ILP_OPTIMAL;
+          nok += st[q] == RGC_ILP_GAP_OK;
+          ntake += take[q];
+        }
+        std::fprintf(stderr, "rgc_ilp fixsearch %d: %lld flagged, %lld eligible, %lld columns; "
+                     "%lld optimal, %lld gap-ok, %lld improved; %lld kept > search limit "
+                     "(largest kept set %lld)\n", depth, (long long)nflag, (long long)nel,
+                     (long long)sub_nc, (long long)nopt, (long long)nok, (long long)ntake,
+                     (long long)nbig, (long long)cmax);
+      }
+      std::vector<uint8_t> seen(ncomp, 0);
+      for (int64_t j = 0; j < nc; ++j) {
+        const int32_t q = fix.comp[j];
+        if (!elig[q]) continue;
+        if (take[q]) x[j] = 0;
+        if (st[q]) exact[j] = st[q];
+        gap[j] = 0.0;
+        if (!seen[q]) {   // the component's gap at its first column
+          seen[q] = 1;
+          gap[j] = g[q];   // (<= the first pass's: the bound is min(L, ...))
+        }
+      }
+      for (int64_t i = 0; i < sub_nc; ++i)
+        if (take[fix.comp[sub_col[i]]] && sx[i]) x[sub_col[i]] = 1;
+    }
+  }
+  return 0;
+}
+
+int rgc_ilp_solve(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact) {
+  if (!c || !in || !x || !exact) return fail("null argument");
+  if (c->pend) return fail("rgc_ilp_solve: a submitted run awaits rgc_wait on this context");
+  HIPCHK(hipSetDevice(c->device));
+  const int64_t nc = in->n_cols, nr = in->n_rows;
+  if (nc < 0 || nc >= INT32_MAX || nr < 0 || nr >= INT32_MAX) return fail("n_cols / n_rows out of range");
+  c->times.clear();
+  c->time_names.clear();
+  c->n_ev = 0;
+  c->timing = (in->flags & RGC_F_TIMING) != 0;
+  if (nc == 0) return 0;
+  std::vector<double> gap(nc);
+  TRY(ilp_solve_rec(c, in, x, exact, gap.data(), 0));
+  if (in->gap) std::memcpy(in->gap, gap.data(), nc * 8);
+  TRY(mark(c, "end"));
+  HIPCHK(hipStreamSynchronize(c->stream));
   if (c->timing) {
     for (int i = 0; i + 1 < c->n_ev; ++i) {
       float ms = 0.f;

@@ -378,11 +378,7 @@ __device__ __forceinline__ void epi_core(const T (&xs)[K], const T (&ys)[K], T B
           I[t++] = overlap(xs[a], ys[a], xs[b], ys[b], B);
       }
   }
-#ifdef RGC_X_EPI_NODEG
-  if (false) {
-#else
   if (!multi) {
-#endif
     // weighted degrees from f32 JIs: f32 operands (2^-24 each) and v_rcp_f32 (1 ulp) give
     // < 4e-7 per JI <= 1, < 5.5e-6 per sum of <= 7 terms with its f32 additions; a maximum
     // clear by 3e-5 is the reference's, anything closer takes the exact f64 pass (ties)
@@ -420,14 +416,7 @@ __device__ __forceinline__ void epi_core(const T (&xs)[K], const T (&ys)[K], T B
 #pragma unroll
     for (int t = 0; t < NE; ++t) nan |= isnan(I[t]);
   }
-#ifdef RGC_X_EPI_NOMED
-  { T acc = I[0];
-#pragma unroll
-    for (int t = 1; t < NE; ++t) acc = acc + I[t];
-    I[NE / 2] = I[NE / 2 - 1] = acc; }
-#else
   mid_n<NE>(I);
-#endif
   if (NE & 1) {
     const double m = (double)I[NE / 2];
     *med = nan ? NAN : m / (two_b2 - m);
@@ -495,14 +484,10 @@ __device__ __forceinline__ void epi_single(const CliqueArgs& A, const int (&mem)
     }
     epi_core<K, float>(xf, yf, (float)B, two_b2, multi, exact, arg, med);
   } else {
-#ifdef RGC_X_EPIF32ONLY
-    *exact = true; *med = 0.0;   // timing experiment: the f64 path's registers out
-#else
     double xs[K], ys[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) { xs[i] = A.x[mem[i]]; ys[i] = A.y[mem[i]]; }
     epi_core<K, double>(xs, ys, B, two_b2, multi, exact, arg, med);
-#endif
   }
 }
 

@@ -21,7 +21,7 @@ constexpr int NW = WG / 64;
 // pointers, so their accesses stay global_load / global_store.
 template <typename T>
 using gptr = __attribute__((address_space(1))) T*;
-#if defined(RGC_X_NODETACH) || defined(RGC_STAMPS)   // timing experiment / stamps build: plain values
+#if defined(RGC_STAMPS)
 template <typename T>
 __device__ __forceinline__ gptr<T> gdetach(T* p) { return (gptr<T>)p; }
 __device__ __forceinline__ double sdetach(double v) { return v; }

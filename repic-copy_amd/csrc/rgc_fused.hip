@@ -55,10 +55,7 @@ struct FusedHdr {
   int E, nodes, cc_cnt, cc_max, target, V, status;
   uint32_t ccur;    // P4 clique-queue cursor
   int tief[2];      // P6: some clique of the chunk needs the order pass (by chunk parity)
-  union {
-    int qslot;      // QG (K = 4): the workgroup's HBM level-tree slot (-1: none, LDS queue)
-    int trifail;    // K = 3: the triangle pass overflowed (p4_tri)
-  };
+  int qslot;        // QG (K = 4): the workgroup's HBM level-tree slot (-1: none, LDS queue)
   int64_t C, base;
 };
 
@@ -424,11 +421,7 @@ __device__ __forceinline__ bool fused_epilogue_main(const FCtx<K>& c, int64_t j,
       mid_n<NE>(Is);
       if (NE & 1) {
         med = (double)Is[NE / 2];
-#ifdef RGC_X_NODIV   // timing experiment only
-        med = med * c.two_b2;
-#else
         med = med / (c.two_b2 - med);
-#endif
       } else {
         const double a = (double)Is[NE / 2 - 1], b = (double)Is[NE / 2];
         med = ((a / (c.two_b2 - a)) + (b / (c.two_b2 - b))) / 2.0;
@@ -511,9 +504,7 @@ __device__ __forceinline__ void fused_epilogue_order(const FCtx<K>& c, int64_t j
 #pragma unroll
     for (int b = a + 1; b < K; ++b) ji[a][b] = jaccard(xs[a], ys[a], xs[b], ys[b], c.B, c.two_b2);
   if (!c.set_order) {
-#ifndef RGC_X_NOINSKEY
     for (int i = 0; i < K; ++i) ins[i] = ins_key<K>(c, mem[i]);
-#endif
   }
   uint32_t top;
   int arg = epi_degree_max<K>(ji, &top);
@@ -840,101 +831,10 @@ __device__ __forceinline__ BfsOut<K> bfs_cliques(const FShared& S, FusedHdr& H, 
   }
 }
 
-// ----------------------------------------------------------------------------- P4 (K = 3)
-// Triangles r < h < t (one box per picker, pairwise adjacent; get_cliques.py:49-56,160-161)
-// in ONE pass, thread per root r (picker-0 position): for each picker-1 neighbour h of r (the
-// first segment [fwd[r], split[r]) of r's sorted list), merge h's sorted forward list (all
-// picker 2) with r's picker-2 segment [split[r], fwd[r+1]); every common t is a triangle.  The
-// first TRI_CACHE triangles of a root stay in registers; a wave reserves the queue slots of
-// all its roots with one LDS atomic (wave prefix sum of the counts), so no workgroup barrier
-// or level tree sits between the roots and their cliques.  Slot records are 8 bytes: (r | h <<
-// 16, t | ordinal << 16), the ordinal being the triangle's rank in its root's lexicographic
-// order, so the output index (root's scanned offset + ordinal) does not depend on the slot.
-// Per-root counts go to cnt[r] for that scan.  Returns false when the queue region or the
-// 15-bit ordinals overflow (the caller then runs the BFS).
-constexpr int TRI_CACHE = 3;
-
-template <int NT>
-__device__ __forceinline__ bool p4_tri(const FShared& S, FusedHdr& H, char* q, int qbytes, int n0,
-                                       bool get_cc, uint32_t target, int tid) {
-  const uint32_t cap = (uint32_t)(qbytes / 8);
-  uint2* rec = reinterpret_cast<uint2*>(q);
-  bool over = false;
-  for (int r0 = 0; r0 < n0; r0 += NT) {   // (uniform trip count: the wave ops below)
-    const int r = r0 + tid;
-    uint32_t cnt = 0, c0 = 0, c1 = 0, c2 = 0;
-    const bool ok = r < n0 && S.fwd[r] < S.fwd[r + 1] && (!get_cc || S.parent[r] == target);
-    int lo1 = 0, hi1 = 0, lo2 = 0, hi2 = 0;
-    if (ok) {
-      lo1 = S.fwd[r];
-      hi1 = S.split[r];
-      lo2 = hi1;
-      hi2 = S.fwd[r + 1];
-    }
-    // walk: fn(h, t) for every triangle of root r, in lexicographic order
-    auto walk = [&](auto&& fn) {
-      for (int e = lo1; e < hi1; ++e) {
-        const int h = S.dst[e];
-        int i = S.fwd[h];
-        const int ie = S.fwd[h + 1];
-        int j = lo2;
-        while (i < ie && j < hi2) {
-          const int a = S.dst[i], b = S.dst[j];
-          if (a == b) fn(h, a);
-          i += a <= b ? 1 : 0;
-          j += b <= a ? 1 : 0;
-        }
-      }
-    };
-    if (lo2 < hi2) {
-      walk([&](int h, int t) {
-        const uint32_t pk = (uint32_t)h | ((uint32_t)t << 16);
-        c0 = cnt == 0 ? pk : c0;
-        c1 = cnt == 1 ? pk : c1;
-        c2 = cnt == 2 ? pk : c2;
-        ++cnt;
-      });
-    }
-    if (r < n0) S.cnt[r] = cnt;
-    // slots for the wave's roots: one LDS atomic per wave
-    const int inc = wave_incl_add32((int)cnt);
-    uint32_t base = 0;
-    if ((tid & 63) == 63 && inc > 0) base = atomicAdd(&H.ccur, (uint32_t)inc);
-    base = (uint32_t)__builtin_amdgcn_readlane((int)base, 63);
-    const uint32_t s0 = base + (uint32_t)(inc - (int)cnt);
-    over |= cnt > 0x7FFFu || s0 + cnt > cap;
-    if (cnt == 0 || s0 + cnt > cap || cnt > 0x7FFFu) continue;
-    auto put = [&](uint32_t o, uint32_t pk) {
-      rec[s0 + o] = make_uint2((uint32_t)r | (pk << 16), (pk >> 16) | (o << 16));
-      S.flags[pk & 0xFFFF] = 3;
-      S.flags[pk >> 16] = 3;
-    };
-    S.flags[r] = 3;
-    put(0, c0);
-    if (cnt > 1) put(1, c1);
-    if (cnt > 2) put(2, c2);
-    if (cnt > TRI_CACHE) {   // rare: the rest by a second walk
-      uint32_t o = 0;
-      walk([&](int h, int t) {
-        if (o >= TRI_CACHE) put(o, (uint32_t)h | ((uint32_t)t << 16));
-        ++o;
-      });
-    }
-  }
-  // any thread's overflow fails the whole micrograph's triangle pass (trifail: 0 since P1)
-  if (over) H.trifail = 1;
-  __syncthreads();
-  return H.trifail == 0;
-}
-
 // P2: boxes with up to FILL_FAST forward edges have their targets kept by the count (the
 // last two in cnt, the first of three in the CC-size slot, zero until P3); the fill writes
 // them without walking the stencil again
-#ifdef RGC_X_T3
-constexpr int FILL_FAST = 3;
-#else
 constexpr int FILL_FAST = 2;
-#endif
 
 // Candidates of a box: the 2x3 cell stencil at its cell in the grid of every HIGHER picker
 // (forward edges only): columns cx, cx + 1 from cx = its column - 1 or its column (by the
@@ -1065,36 +965,6 @@ __device__ __forceinline__ int pairs_count_int(const Stencil& st, const FShared&
   uint32_t mask = 0, pk = 0, first = 0;
   int cnt = 0, kk = 0;
   const float ax = (float)st.a.x, ay = (float)st.a.y;
-#ifdef RGC_X_P2A
-  // every stencil range of every higher picker first (one batch of LDS reads), then one
-  // non-unrolled candidate loop per range
-  constexpr int NR = 2 * (K - 1);
-  int lo[NR], hi[NR];
-#pragma unroll
-  for (int qi = 0; qi < K - 1; ++qi)
-#pragma unroll
-    for (int d = 0; d < 2; ++d) {
-      int l = 0, h = 0;
-      if (qi + 1 > st.p) stencil_range(st, S, H, qi + 1, d, l, h);
-      lo[qi * 2 + d] = l;
-      hi[qi * 2 + d] = h;
-    }
-#pragma unroll
-  for (int r = 0; r < NR; ++r) {
-#pragma unroll 1
-    for (int t = lo[r]; t < hi[r]; ++t, ++kk) {
-      const float2 bf = reinterpret_cast<const float2*>(S.sxy)[t];
-      const float xo = fmaxf(Bf - fabsf(ax - bf.x), 0.0f);
-      const float yo = fmaxf(Bf - fabsf(ay - bf.y), 0.0f);
-      if (xo * yo > Tf) {
-        first = cnt == 0 ? (uint32_t)t : first;
-        ++cnt;
-        mask |= (kk < 32) ? (1u << kk) : 0u;
-        pk = (pk << 16) | (uint32_t)t;
-      }
-    }
-  }
-#else
   for (int q = st.p + 1; q < K; ++q) {
 #pragma unroll
     for (int d = 0; d <= 1; ++d) {
@@ -1113,7 +983,6 @@ __device__ __forceinline__ int pairs_count_int(const Stencil& st, const FShared&
       }
     }
   }
-#endif
   *mask_out = cnt <= FILL_FAST ? pk : mask;
   *first_out = first;
   return cnt;
@@ -1176,13 +1045,9 @@ __device__ __forceinline__ void put_stats(const FusedArgs& A, int m, int status,
 // Waves per SIMD the register allocator targets.  K = 3 fits 64 VGPRs (4 small spills) for 8
 // waves per SIMD = 4 workgroups per CU, which the f32-coordinate LDS layout also allows; larger
 // K keep the compiler's choice (their VGPRs, not LDS, bound the occupancy).
-#ifdef RGC_X_NOWPE   // timing experiment: compiler's own register budget
-constexpr int fused_waves_per_eu(int, int) { return 1; }
-#else
 constexpr int fused_waves_per_eu(int k, int nt) {
   return nt == 1024 ? 4 : (nt == 768 ? 6 : (nt == 256 ? 4 : (nt == 384 ? 6 : (k <= 3 ? 8 : 1))));
 }
-#endif
 
 // HBM level-tree slots (QG launches): claim a free bit of the slot bitmap (one thread), or -1
 // after a bounded search (then the workgroup keeps the LDS queue).  There are twice as many
@@ -1415,7 +1280,7 @@ void k_fused(FusedArgs A) {
       H.status = (!W && mnx == -INFINITY) ? RGC_ST_DEFER_WIDE : 0;
       H.C = 0; H.base = 0; H.V = 0; H.target = -1; H.ccur = 0;
       H.tief[0] = H.tief[1] = 0;
-      H.qslot = 0;   // (= trifail)
+      H.qslot = 0;
     }
   }
   __syncthreads();
@@ -1532,11 +1397,7 @@ void k_fused(FusedArgs A) {
     // fill each list (already sorted: position order) and record each edge's source in dst's
     // unused tail when it has room; then union the edges one thread per edge (lock-free
     // union-find, balanced across lanes whatever the degrees).  Without room: union per box.
-#ifdef RGC_X_BOXUNION   // experiment: union per box inside the fill
-    const bool src_ok = false;
-#else
     const bool src_ok = 2 * E <= A.ecap || (QG && esrc_g != nullptr);
-#endif
     uint16_t* esrc = S.dst + E;
     // (QG: esrc_g in HBM when dst's tail is short; separate loops keep esrc's LDS accesses
     // ds_* instructions instead of flat ones)
@@ -1609,9 +1470,7 @@ void k_fused(FusedArgs A) {
       for (int e = tid; e < E; e += FWG) {
         const uint32_t h = S.dst[e];
         S.flags[h] = 1;
-#ifndef RGC_X_NOUNION   // timing experiment only: no unions (CC stats wrong)
         uf_union32(S.cnt, esrc[e], h);
-#endif
       }
       __syncthreads();
     }
@@ -1758,20 +1617,7 @@ void k_fused(FusedArgs A) {
   BfsOut<K> bo;
   int nch = 0;
   int64_t C = 0;
-  // K = 3: one-pass triangle listing into the LDS queue (p4_tri); the BFS below only when its
-  // queue overflowed
-  bool tri = false;
-  if constexpr (K == 3) {
-#ifdef RGC_X_TRI   // (slower than the BFS on C2 and C4: profiles/r04f_ab_*)
-    tri = p4_tri<NT>(S, H, q, qbytes, n0, get_cc, (uint32_t)target, tid);
-#endif
-    if (tri) {
-      C = block_scan_dpp<FWG>(S.cnt, n0, H.red64);   // root offsets (output order)
-      nch = 1;
-      bo.C = C;
-    }
-  }
-  if (!tri) {
+  {
     int r0 = 0, len = n0;
     bool ok = maxch >= 1;
     if (tid == 0) { chtab[0] = 0; chtab[1] = 0; }
@@ -1801,9 +1647,7 @@ void k_fused(FusedArgs A) {
     if (!ok) { nch = 0; C = 0; bo.C = -1; }
   }
   const bool bfs_ok = nch > 0;
-  if (tri) {
-    c.cq_cap = (int)max(C, (int64_t)1);   // slot records in q (P6 reads them)
-  } else if (bfs_ok) {
+  if (bfs_ok) {
     // cliques = level-K tree entries (members by walking parents); their flag words follow
     c.cq_cap = (int)max(bo.C, (int64_t)1);
     c.cq_ord = reinterpret_cast<uint16_t*>(q + bo.lvl[K] + (we ? 8 : 4) * (int)bo.C);
@@ -1817,9 +1661,7 @@ void k_fused(FusedArgs A) {
         int mem[K];
         mem[0] = r;
         c.count = 0;
-#ifndef RGC_X_NODFS
         FLevel<K, 1, false>::run(c, mem);
-#endif
         cntr = (uint32_t)c.count;
       }
       S.cnt[r] = cntr;
@@ -1849,23 +1691,11 @@ void k_fused(FusedArgs A) {
     } else if (C > 0x7fffffff) {
       H.status = RGC_ST_DEFER;   // P6 indexes a micrograph's cliques in 32 bits
     } else {
-#ifdef RGC_X_NORESV   // timing experiment: no contended reservation (outputs overlap)
-      resv = (unsigned long long)min((int64_t)blockIdx.x * (A.cap / (int64_t)gridDim.x), A.cap - C);
-#elif defined(RGC_X_RSHARD)   // timing experiment: 8 cursor words 256 B apart (outputs overlap)
-      int vz;
-      asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
-      // (counters in the unused tail of the rows array)
-      // (64-byte aligned: a misaligned 64-bit atomic faults)
-      unsigned long long* ctr = reinterpret_cast<unsigned long long*>(
-          reinterpret_cast<uintptr_t>(A.rows + (A.cap * K - 8192)) & ~(uintptr_t)63);
-      resv = atomicAdd(ctr + 64 * (blockIdx.x & 7) + vz, (unsigned long long)C) % (A.cap / 2);
-#else
       // (a lane-varying zero offset keeps the atomic optimizer's wave-reduction expansion,
       // which consumes the result at once, off this single-lane atomic)
       int vz;
       asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
       resv = atomicAdd(A.cursor + vz, (unsigned long long)C);
-#endif
     }
   }
   __syncthreads();
@@ -1962,10 +1792,7 @@ void k_fused(FusedArgs A) {
     for (int ci = 0; ci < nit; ++ci) {
       int c0, c1;
       if (tid == 0) H.tief[(ci + 1) & 1] = 0;   // last read before the previous chunk's end
-      if (tri) {
-        c0 = 0;
-        c1 = Cm;
-      } else if (bfs_ok) {
+      if (bfs_ok) {
         const int ch = ci == 0 ? nch - 1 : ci - 1;
         c0 = ufl((int)chtab[2 * ch + 1]);
         c1 = ufl((int)chtab[2 * ch + 3]);
@@ -1990,23 +1817,13 @@ void k_fused(FusedArgs A) {
           int mem[K];
           mem[0] = r;
           c.out = lo;
-#ifndef RGC_X_NODFS
           FLevel<K, 1, true>::run(c, mem);
-#endif
         }
         __syncthreads();
       }
-      // members of chunk slot sl: triangle record, BFS tree walk, or the re-walk buffer; the
-      // output index of the slot; the order-pass flag of the slot
-      uint2* trec = reinterpret_cast<uint2*>(q);
+      // members of chunk slot sl: BFS tree walk or the re-walk buffer; the output index of
+      // the slot; the order-pass flag of the slot
       auto clique_members = [&](int sl, int (&mem)[K]) -> int64_t {
-        if (tri) {
-          const uint2 rr = trec[sl];
-          mem[0] = (int)(rr.x & 0xFFFF);
-          mem[1] = (int)(rr.x >> 16);
-          mem[K - 1] = (int)(rr.y & 0xFFFF);
-          return obase + (int64_t)(S.cnt[mem[0]] + ((rr.y >> 16) & 0x7FFF));
-        }
         if (bfs_ok) {
           if (we) BfsLevel<K, K, NT, QG && K <= 4>::prefix(q, cur.lvl, (uint32_t)sl, mem);
           else BfsLevel<K, K, NT>::prefix(q, cur.lvl, (uint32_t)sl, mem);
@@ -2018,21 +1835,15 @@ void k_fused(FusedArgs A) {
         return obase + (c0 + sl);
       };
       auto set_order_flag = [&](int sl) {
-        if (tri) reinterpret_cast<uint32_t*>(trec)[2 * sl + 1] |= 0x80000000u;
-        else c.cq_ord[sl] |= 0x8000;
+        c.cq_ord[sl] |= 0x8000;
       };
       auto order_flag = [&](int sl) -> bool {
-        if (tri) return (trec[sl].y & 0x80000000u) != 0;
         return (c.cq_ord[sl] & 0x8000) != 0;
       };
       bool any = false;
       for (int sl = tid; sl < c1 - c0; sl += FWG) {
         int mem[K];
         const int64_t jo = clique_members(sl, mem);
-#ifdef RGC_X_NOEPI   // timing experiment only: members walked, no epilogue
-        if (mem[0] == 0xFFFFF) c.cq_ord[sl] = 1;
-        continue;
-#endif
         bool order;
         if constexpr (!W) order = fused_epilogue_main<K, W, true>(c, jo, mem);
         else order = fused_epilogue_main<K, W, false>(c, jo, mem);
@@ -2043,11 +1854,7 @@ void k_fused(FusedArgs A) {
       }
       if (any) H.tief[ci & 1] = 1;
       __syncthreads();
-#ifdef RGC_X_NOORDER   // timing experiment only: no order pass (tie consensus wrong)
-      if (false) {
-#else
       if (H.tief[ci & 1]) {
-#endif
         for (int sl = tid; sl < c1 - c0; sl += FWG) {
           if (!order_flag(sl)) continue;
           int mem[K];

@@ -27,7 +27,6 @@ namespace rgc {
 
 constexpr int ILP_WG = 256;
 constexpr uint8_t ST_IN_SEED = 1;        // (= ST_IN below: the pre-search packing)
-constexpr uint8_t ILP_UNSEARCHED = 255;  // wave component skipped past the time budget
 constexpr int ILP_SMALL = 64;     // thread-per-component limit (one 64-bit mask)
 constexpr int ILP_BIG = 4096;     // wave-per-component limit (64 lanes x 64 bits)
 // the wave search stops at Gurobi's MIPGap (GAP_OK) only after this many nodes: a component
@@ -304,17 +303,12 @@ __global__ __launch_bounds__(64) void k_ilp_wave(IlpArgs A, int n_big) {
   __shared__ int counter;
   const int lane = threadIdx.x;
   uint64_t* base = A.wscratch + (int64_t)blockIdx.x * A.wstride;
-  // (the launch's waves are all resident at once: each one's start is the launch's)
-  const uint64_t deadline =
-      A.wave_budget ? (uint64_t)__builtin_amdgcn_s_memrealtime() + A.wave_budget : 0;
   for (int bi = blockIdx.x; bi < n_big; bi += gridDim.x) {
     const int64_t comp = A.big[bi];
     const int n = A.comp_n[comp];
     int32_t* m = A.members + A.comp_off[comp];
-    // past the launch's time budget: not searched (the certification packs it: ST_UNSEARCHED)
-    const bool late = deadline && (uint64_t)__builtin_amdgcn_s_memrealtime() > deadline;
-    if (n > ILP_BIG || late) {
-      for (int i = lane; i < n; i += 64) { A.x[m[i]] = 0; A.exact[m[i]] = late ? ILP_UNSEARCHED : 0; }
+    if (n > ILP_BIG) {
+      for (int i = lane; i < n; i += 64) { A.x[m[i]] = 0; A.exact[m[i]] = 0; }
       continue;
     }
     const int W = (n + 63) / 64;
@@ -488,18 +482,14 @@ __global__ __launch_bounds__(64) void k_ilp_wave(IlpArgs A, int n_big) {
     int64_t nodes = 0;
     uint8_t status = RGC_ILP_OPTIMAL;
     // node budget in work units: a node costs O(W) (bound passes over P's words), so
-    // components above 1024 cliques get node_limit * 16 / W nodes (a whole C5 micrograph's
-    // medium components ran 27 s at 2^22 nodes each)
+    // components above 1024 cliques get node_limit * 16 / W nodes.  The budget is the only
+    // limit of the search (no clock): the result does not depend on the device's speed or load
     const int64_t node_cap = A.node_limit * 16 / (W > 16 ? W : 16);
     for (; status == RGC_ILP_OPTIMAL;) {
       bool back = false;
       if (++nodes > node_cap) { status = RGC_ILP_NODE_LIMIT; break; }
-      // the launch's time budget, and past ILP_GAP_NODES the MIPGap stop, every 1024 nodes
+      // past ILP_GAP_NODES the MIPGap stop, checked every 1024 nodes
       if ((nodes & 1023) == 0) {
-        if (deadline && (uint64_t)__builtin_amdgcn_s_memrealtime() > deadline) {
-          status = RGC_ILP_NODE_LIMIT;
-          break;
-        }
         if (nodes >= ILP_GAP_NODES && best > 0.0 && root_bound - best <= 1e-4 * best) {
           status = RGC_ILP_GAP_OK;
           break;
@@ -598,6 +588,24 @@ constexpr uint8_t ST_UND = 0, ST_IN = 1, ST_OUT = 2, ST_NONE = 3;
 constexpr int CS = 10;  // doubles per component record: lsum g2 lbest mu primal step stall flag
                         // repacked-primal (spare)
 
+// Per-component sums of f64 terms over many columns / rows (the Lagrangian value and the
+// packing values, slots 0, 4 and 8 of the record) are accumulated in fixed point, 2^-32
+// units in an int64, so the result does not depend on the order of the atomics: the whole
+// solve is deterministic (two runs give the same x).  Terms of the dual bound round up and
+// terms of a packing value round down, so certified gaps stay valid (the slack is 2^-32 per
+// term: < 2e-4 absolute over a 705k-clique micrograph, 1.5e-7 of its objective).
+constexpr double FX_ONE = 4294967296.0;
+__device__ __forceinline__ void fx_add_up(double* slot, double v) {
+  atomicAdd(reinterpret_cast<unsigned long long*>(slot), (unsigned long long)(long long)ceil(v * FX_ONE));
+}
+__device__ __forceinline__ void fx_add_dn(double* slot, double v) {
+  atomicAdd(reinterpret_cast<unsigned long long*>(slot), (unsigned long long)(long long)floor(v * FX_ONE));
+}
+__device__ __forceinline__ long long fx_raw(const double* slot) {
+  return *reinterpret_cast<const long long*>(slot);
+}
+__device__ __forceinline__ double fx_get(const double* slot) { return (double)fx_raw(slot) / FX_ONE; }
+
 __device__ __forceinline__ int64_t ilp_comp(const IlpArgs& A, int64_t c) {
   return A.comp_id[A.parent[c]];
 }
@@ -612,7 +620,7 @@ __global__ __launch_bounds__(ILP_WG) void k_cert_flag(IlpArgs A) {
   const int n = A.comp_n[comp];
   uint8_t f = 0;
   const uint8_t ex = n > 1 ? A.exact[A.members[A.comp_off[comp]]] : 1;
-  if (n > ILP_BIG || ex == ILP_UNSEARCHED) f = 2;
+  if (n > ILP_BIG) f = 2;
   else if (ex == 0) f = 1;
   A.cert[comp] = f;
   if (f) atomicAdd(A.count + 1, 1u);   // flagged components (the host skips the rest when 0)
@@ -767,7 +775,7 @@ __global__ __launch_bounds__(ILP_WG) void k_lr_init(IlpArgs A) {
   const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
   if (c >= A.n_cols || A.st[c] == ST_NONE) return;
   const int64_t comp = ilp_comp(A, c);
-  if (A.st[c] == ST_IN) atomicAdd(A.cs + comp * CS + 4, A.w[c]);
+  if (A.st[c] == ST_IN) fx_add_dn(A.cs + comp * CS + 4, A.w[c]);
   const double share = fmax(A.w[c], 0.0) / (double)(A.col_ptr[c + 1] - A.col_ptr[c]);
   for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e)
     atomicMax(reinterpret_cast<unsigned long long*>(A.lam + A.row_idx[e]),
@@ -780,7 +788,7 @@ __global__ __launch_bounds__(ILP_WG) void k_lr_cols(IlpArgs A) {
   double rc = A.w[c];
   for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e) rc -= A.lam[A.row_idx[e]];
   if (!(rc > 0.0)) return;
-  atomicAdd(A.cs + ilp_comp(A, c) * CS + 0, rc);
+  fx_add_up(A.cs + ilp_comp(A, c) * CS + 0, rc);
   for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e) atomicAdd(A.grad + A.row_idx[e], 1.0);
 }
 __global__ __launch_bounds__(ILP_WG) void k_lr_rows(IlpArgs A) {
@@ -792,14 +800,14 @@ __global__ __launch_bounds__(ILP_WG) void k_lr_rows(IlpArgs A) {
   if (A.lam[r] <= 0.0 && g > 0.0) g = 0.0;   // projected: lam stays at 0
   A.grad[r] = g;
   double* cs = A.cs + comp * CS;
-  atomicAdd(cs + 0, A.lam[r]);
-  atomicAdd(cs + 1, g * g);
+  fx_add_up(cs + 0, A.lam[r]);
+  atomicAdd(cs + 1, g * g);   // (integers: exact in any order)
 }
 __global__ __launch_bounds__(ILP_WG) void k_lr_step(IlpArgs A) {
   const int64_t comp = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
   if (comp >= A.n_comp || A.cert[comp] == 0) return;
   double* cs = A.cs + comp * CS;
-  const double L = cs[0], g2 = cs[1], P = cs[4];
+  const double L = fx_get(cs + 0), g2 = cs[1], P = fx_get(cs + 4);
   // cs[7]: 1 = this lam is the best so far (rows keep a copy), 2 = restart from that copy
   cs[7] = 0.0;
   if (!(L >= cs[2] - 1e-9 * fabs(cs[2]))) {   // (first iteration: cs[2] = inf)
@@ -866,7 +874,7 @@ __global__ __launch_bounds__(ILP_WG) void k_rp_primal(IlpArgs A) {
   const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
   if (c >= A.n_cols || A.st[c] != ST_IN) return;
   const int64_t comp = ilp_comp(A, c);
-  if (A.cert[comp] != 0) atomicAdd(A.cs + comp * CS + 8, A.w[c]);
+  if (A.cert[comp] != 0) fx_add_dn(A.cs + comp * CS + 8, A.w[c]);
 }
 // keep the better packing per component (ties: the earlier one)
 __global__ __launch_bounds__(ILP_WG) void k_rp_pick(IlpArgs A) {
@@ -875,13 +883,13 @@ __global__ __launch_bounds__(ILP_WG) void k_rp_pick(IlpArgs A) {
   const int64_t comp = ilp_comp(A, c);
   if (A.cert[comp] == 0) return;
   const double* cs = A.cs + comp * CS;
-  if (!(cs[8] > cs[4])) A.st[c] = A.st_save[c];
+  if (!(fx_raw(cs + 8) > fx_raw(cs + 4))) A.st[c] = A.st_save[c];
 }
 __global__ __launch_bounds__(ILP_WG) void k_rp_comps(IlpArgs A) {
   const int64_t comp = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
   if (comp >= A.n_comp || A.cert[comp] == 0) return;
   double* cs = A.cs + comp * CS;
-  cs[4] = fmax(cs[4], cs[8]);
+  if (fx_raw(cs + 8) > fx_raw(cs + 4)) cs[4] = cs[8];   // (fixed-point bits)
   cs[8] = 0.0;
 }
 // rows: the best multipliers back where the subgradient's restarts read them
@@ -901,7 +909,7 @@ __global__ __launch_bounds__(ILP_WG) void k_cert_final(IlpArgs A) {
   const int64_t comp = ilp_comp(A, c);
   const double* cs = A.cs + comp * CS;
   A.x[c] = A.st[c] == ST_IN ? 1 : 0;
-  const double P = cs[4], Lb = cs[2];
+  const double P = fx_get(cs + 4), Lb = cs[2];
   const bool ok = Lb - P <= 1e-4 * fabs(P);
   A.exact[c] = ok ? RGC_ILP_GAP_OK : (A.cert[comp] == 2 ? RGC_ILP_HEURISTIC : RGC_ILP_NODE_LIMIT);
   // the component's absolute gap, once (at its first column), for micrograph-level MIPGap
@@ -911,6 +919,62 @@ __global__ __launch_bounds__(ILP_WG) void k_cert_final(IlpArgs A) {
 __global__ __launch_bounds__(ILP_WG) void k_cert_reset_primal(IlpArgs A) {
   const int64_t comp = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
   if (comp < A.n_comp) A.cs[comp * CS + 4] = 0.0;
+}
+
+// ------------------------------------------------------------------ reduced-cost fixing
+// After the certification, a flagged component has a packing P and multipliers lam (the best
+// ones, in rmax) with dual bound L(lam) = sum_r lam_r + sum_c max(0, rc_c), rc_c = w_c -
+// sum_{r in c} lam_r.  Fixing x_c = 1 in the Lagrangian gives: every packing that contains
+// column c is worth at most L + min(0, rc_c).  So a column with rc_c <= P - L cannot be part
+// of a packing better than P, and the component's optimum is max(P, optimum over the kept
+// columns rc_c > P - L).  These models are nearly integral with few rows per component
+// (dense clusters: 17-54 boxes, up to 79k cliques, in a crowded C5 micrograph), and the
+// columns within the bound's gap of zero reduced cost are a few hundred: that restricted
+// problem is small enough for the exact search (rgc_ilp_solve runs it as a second pass).
+// L and P are recomputed here in fixed point (L rounded up, P down), so the kept set is a
+// superset of what exact arithmetic would keep; the packing's own columns are always kept.
+__global__ __launch_bounds__(ILP_WG) void k_fs_init(IlpArgs A) {
+  const int64_t comp = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (comp >= A.n_comp) return;
+  A.fs[2 * comp] = 0.0;
+  A.fs[2 * comp + 1] = 0.0;
+  A.fs_cnt[comp] = 0;
+}
+__global__ __launch_bounds__(ILP_WG) void k_fs_rows(IlpArgs A) {
+  const int64_t r = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (r >= A.n_rows) return;
+  const int64_t comp = ilp_row_comp(A, r);
+  if (comp < 0 || A.cert[comp] == 0) return;
+  fx_add_up(A.fs + 2 * comp, reinterpret_cast<const double*>(A.rmax)[r]);
+}
+__device__ __forceinline__ double fs_rc(const IlpArgs& A, int64_t c) {
+  const double* lam = reinterpret_cast<const double*>(A.rmax);
+  double rc = A.w[c];
+  for (int64_t e = A.col_ptr[c]; e < A.col_ptr[c + 1]; ++e) rc -= lam[A.row_idx[e]];
+  return rc;
+}
+__global__ __launch_bounds__(ILP_WG) void k_fs_cols(IlpArgs A) {
+  const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (c >= A.n_cols) return;
+  const int64_t comp = ilp_comp(A, c);
+  A.loc[c] = (int32_t)comp;   // (the solvers' local numbering is dead: the host maps columns)
+  A.fs_keep[c] = 0;
+  if (A.cert[comp] == 0) return;
+  const double rc = fs_rc(A, c);
+  if (rc > 0.0) fx_add_up(A.fs + 2 * comp, rc);
+  if (A.st[c] == ST_IN) fx_add_dn(A.fs + 2 * comp + 1, A.w[c]);
+}
+__global__ __launch_bounds__(ILP_WG) void k_fs_keep(IlpArgs A) {
+  const int64_t c = (int64_t)blockIdx.x * ILP_WG + threadIdx.x;
+  if (c >= A.n_cols) return;
+  const int64_t comp = A.loc[c];
+  if (A.cert[comp] == 0) return;
+  const double L = fx_get(A.fs + 2 * comp), P = fx_get(A.fs + 2 * comp + 1);
+  // (a relative 1e-12 of slack for the f64 rounding of rc)
+  const bool keep = A.st[c] == ST_IN || fs_rc(A, c) > P - L - 1e-12 * (1.0 + fabs(L));
+  if (!keep) return;
+  A.fs_keep[c] = 1;
+  atomicAdd(A.fs_cnt + comp, 1u);
 }
 
 void launch_ilp_cert(hipStream_t stream, int phase, const IlpArgs& A) {
@@ -967,6 +1031,12 @@ void launch_ilp_cert(hipStream_t stream, int phase, const IlpArgs& A) {
       RGC_L(k_rp_pick, nbc);
       RGC_L(k_rp_comps, nbk);
       if (nbr) RGC_L(k_rp_best, nbr);
+      break;
+    case 10:  // reduced-cost fixing: dual bound and packing value, then the kept columns
+      RGC_L(k_fs_init, nbk);
+      if (nbr) RGC_L(k_fs_rows, nbr);
+      RGC_L(k_fs_cols, nbc);
+      RGC_L(k_fs_keep, nbc);
       break;
   }
 #undef RGC_L

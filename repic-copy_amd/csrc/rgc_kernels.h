@@ -226,7 +226,7 @@ int64_t scan_tiles_needed(int64_t n);
 // SCAN_EPOCH_REFRESH launches must be zeroed before its next scan (launch epochs repeat after
 // 2^22 - 1 launches)
 constexpr uint32_t SCAN_EPOCH_REFRESH = 1u << 20;
-uint32_t scan_epoch_count();
+uint64_t scan_epoch_count();
 void launch_scan(hipStream_t stream, int64_t n, const int32_t* in, int64_t* out,
                  int64_t* tile_buf, int64_t* total);
 void launch_cc(hipStream_t stream, int phase, int N, int n_mg, int k, int get_cc,
@@ -318,9 +318,12 @@ struct IlpArgs {
   unsigned int* count;        // round counter
   double* gap;                // optional [n_cols]: component bound - packing at its first column
   uint8_t* st_save;           // [n_cols] certification: the packing before a Lagrangian repack
-  uint64_t wave_budget;       // wave search: s_memrealtime ticks (100 MHz) after its start past
-                              // which no new component is searched and running searches stop
-                              // (0: none)
+  // reduced-cost fixing (rgc_ilp.hip k_fs_*): per component the dual bound and packing value
+  // of the certification (fixed point, fs[2 comp], fs[2 comp + 1]) and the number of columns
+  // kept (fs_cnt); per column the kept flag
+  double* fs;
+  unsigned int* fs_cnt;
+  uint8_t* fs_keep;
 };
 int ilp_small_max();
 int ilp_big_max();

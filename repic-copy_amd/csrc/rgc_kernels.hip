@@ -300,76 +300,8 @@ __global__ __launch_bounds__(WG) void k2_pairs(int N, int k, double B, double tw
 }
 
 // ----------------------------------------------------------------------------- scan
-// Exclusive scan of int32 counts into int64 offsets (out[n] = total), three launches.
-__global__ __launch_bounds__(WG) void scan_tiles(int64_t n, const int32_t* __restrict__ in,
-                                                 int64_t* tile_sum) {
-  __shared__ int64_t red[NW];
-  const int64_t t0 = (int64_t)blockIdx.x * SCAN_TILE;
-  int64_t s = 0;
-  for (int i = threadIdx.x; i < SCAN_TILE; i += WG) {
-    const int64_t j = t0 + i;
-    if (j < n) s += in[j];
-  }
-  s = block_sum64(s, red);
-  if (threadIdx.x == 0) tile_sum[blockIdx.x] = s;
-}
-
-__global__ __launch_bounds__(1024) void scan_sums(int64_t nt, int64_t* tile_sum, int64_t* total) {
-  __shared__ int64_t lds[16];
-  __shared__ int64_t carry;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (int64_t b = 0; b < nt; b += 1024) {
-    const int64_t j = b + threadIdx.x;
-    const int64_t v = j < nt ? tile_sum[j] : 0;
-    const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int64_t inc = v;
-    for (int o = 1; o < 64; o <<= 1) {
-      int64_t t = __shfl_up(inc, o, 64);
-      if (l >= o) inc += t;
-    }
-    if (l == 63) lds[w] = inc;
-    __syncthreads();
-    int64_t pre = 0, tot = 0;
-    for (int i = 0; i < 16; ++i) {
-      if (i < w) pre += lds[i];
-      tot += lds[i];
-    }
-    const int64_t c = carry;
-    if (j < nt) tile_sum[j] = c + pre + inc - v;
-    __syncthreads();
-    if (threadIdx.x == 0) carry = c + tot;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) *total = carry;
-}
-
-__global__ __launch_bounds__(WG) void scan_apply(int64_t n, const int32_t* __restrict__ in,
-                                                 const int64_t* __restrict__ tile_off,
-                                                 const int64_t* __restrict__ total,
-                                                 int64_t* out) {
-  __shared__ int64_t red[NW];
-  constexpr int PER = SCAN_TILE / WG;
-  const int64_t t0 = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * PER;
-  int32_t v[PER];
-  int64_t s = 0;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    v[i] = (t0 + i < n) ? in[t0 + i] : 0;
-    s += v[i];
-  }
-  int64_t tot;
-  int64_t pre = block_excl_scan(s, red, &tot) + tile_off[blockIdx.x];
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    if (t0 + i < n) out[t0 + i] = pre;
-    pre += v[i];
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = *total;
-}
-
-// Single-pass exclusive scan (decoupled look-back): one launch instead of scan_tiles +
-// scan_sums + scan_apply, reading the counts once and writing the offsets once.  Tiles of
+// Exclusive scan of int32 counts into int64 offsets (out[n] = total) in a single pass
+// (decoupled look-back), reading the counts once and writing the offsets once.  Tiles of
 // ONE_TILE counts are claimed in order on a counter (a tile's predecessors are then already
 // running or done, whatever the dispatch order); each tile publishes its aggregate, looks back
 // over its predecessors' published states (one wave, 64 states per step) for the exclusive
@@ -434,7 +366,8 @@ __global__ __launch_bounds__(WG) void scan_onepass(int64_t n, const int32_t* __r
     if (lane == 0) st_store(state + tile, (tile == 0 ? ST_INC : ST_AGG) | ep | (uint64_t)agg);
     int64_t excl = 0;
     int j = tile - 1;   // the highest predecessor not yet folded in
-    for (int guard = 0; j >= 0 && guard < (1 << 24); ++guard) {
+    bool done = j < 0;
+    for (int guard = 0; !done && guard < (1 << 24); ++guard) {
       const int idx = j - lane;
       uint64_t w = idx >= 0 ? st_load(state + idx) : (ST_INC | ep);   // (before tile 0: 0)
       const bool ready = (w & ep_mask()) == ep && (w >> 62) != 0;
@@ -445,16 +378,24 @@ __global__ __launch_bounds__(WG) void scan_onepass(int64_t n, const int32_t* __r
       int64_t val = (lane <= first && idx >= 0) ? (int64_t)(w & ST_VAL) : 0;
       for (int o = 32; o > 0; o >>= 1) val += __shfl_xor(val, o, 64);
       excl += val;
-      if (inc) break;
       j -= 64;
+      done = inc != 0 || j < 0;
     }
     if (lane == 0) {
-      if (tile > 0) st_store(state + tile, ST_INC | ep | (uint64_t)(excl + agg));
-      s_pre = excl;
-      if (tile == ntiles - 1) {
-        out[n] = excl + agg;
-        *total = excl + agg;
+      if (!done) {
+        // look-back guard exhausted (a predecessor never published: a stale tile buffer):
+        // no prefix is published, and the totals read -1 so the host's check of the total
+        // fails instead of sizing allocations from a wrong prefix
+        out[n] = -1;
+        *total = -1;
+      } else {
+        if (tile > 0) st_store(state + tile, ST_INC | ep | (uint64_t)(excl + agg));
+        if (tile == ntiles - 1) {
+          out[n] = excl + agg;
+          *total = excl + agg;
+        }
       }
+      s_pre = excl;
     }
   }
   __syncthreads();
@@ -969,29 +910,21 @@ void launch_pairs(hipStream_t stream, bool fill, int N, int k, double B, double 
                sx, sy, sbox, spick, smg, fwd_cnt, fwd_off, e_dst, e_ji);
 }
 
-// tile buffer words: the one-pass scan's claim counter + one state per tile (the three-launch
-// scan's tile sums fit the same words)
+// tile buffer words: the one-pass scan's claim counter + one state per tile
 int64_t scan_tiles_needed(int64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 2; }
 
-static std::atomic<uint32_t> g_scan_epochs{0};
-uint32_t scan_epoch_count() { return g_scan_epochs.load(); }
+// (64-bit: the count never wraps, so an epoch value recurs exactly every 2^22 - 1 launches)
+static std::atomic<uint64_t> g_scan_epochs{0};
+uint64_t scan_epoch_count() { return g_scan_epochs.load(); }
 
 void launch_scan(hipStream_t stream, int64_t n, const int32_t* in, int64_t* out,
                  int64_t* tile_buf, int64_t* total) {
-#ifdef RGC_X_SCAN3   // the three-launch scan (A/B timing)
-  const int64_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
-  if (nt > 0) RGC_LAUNCH(scan_tiles, nt, WG, n, in, tile_buf + 1);
-  RGC_LAUNCH(scan_sums, 1, 1024, nt, tile_buf + 1, total);
-  if (nt > 0) RGC_LAUNCH(scan_apply, nt, WG, n, in, tile_buf + 1, total, out);
-  else (void)hipMemcpyAsync(out, total, sizeof(int64_t), hipMemcpyDeviceToDevice, stream);
-#else
   // launch epochs are process-wide (any two launches sharing a tile buffer differ; an epoch
   // repeats after 2^22 - 1 launches, so the owner of a tile buffer zeroes it at least every
   // SCAN_EPOCH_REFRESH launches: scan_epoch_count)
-  const uint32_t e = g_scan_epochs.fetch_add(1) % ((1u << 22) - 1) + 1;
+  const uint32_t e = (uint32_t)(g_scan_epochs.fetch_add(1) % ((1u << 22) - 1)) + 1;
   const int64_t nt = std::max<int64_t>(1, (n + ONE_TILE - 1) / ONE_TILE);
   RGC_LAUNCH(scan_onepass, nt, WG, n, in, out, total, reinterpret_cast<uint64_t*>(tile_buf), e);
-#endif
 }
 
 void launch_cc(hipStream_t stream, int phase, int N, int n_mg, int k, int get_cc,

@@ -78,6 +78,7 @@ lib.rgc_last_error.restype = C.c_char_p
 lib.rgc_device_count.argtypes = [C.POINTER(C.c_int)]
 lib.rgc_ctx_create.argtypes = [C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]
 lib.rgc_ctx_destroy.argtypes = [C.c_void_p]
+lib.rgc_ctx_set_copy_stream.argtypes = [C.c_void_p, C.c_void_p]
 lib.rgc_ctx_destroy.restype = None
 lib.rgc_run.argtypes = [C.c_void_p, C.POINTER(BatchIn), C.POINTER(BatchOut)]
 lib.rgc_submit.argtypes = [C.c_void_p, C.POINTER(BatchIn)]
@@ -108,7 +109,7 @@ lib.rgc_pickle_bytes.argtypes = [C.POINTER(PickleFmt), C.POINTER(WriteIn), C.c_i
 lib.rgc_py_float_repr.argtypes = [C.c_double, C.c_char_p, C.c_int]
 
 EXPORTS = ["rgc_abi_version", "rgc_last_error", "rgc_device_count", "rgc_ctx_create",
-           "rgc_ctx_destroy", "rgc_run", "rgc_submit", "rgc_wait", "rgc_fetch_stats", "rgc_detach_host", "rgc_host_block_free", "rgc_kernel_times", "rgc_last_edges", "rgc_parse_files",
+           "rgc_ctx_destroy", "rgc_ctx_set_copy_stream", "rgc_run", "rgc_submit", "rgc_wait", "rgc_fetch_stats", "rgc_detach_host", "rgc_host_block_free", "rgc_kernel_times", "rgc_last_edges", "rgc_parse_files",
            "rgc_parsed_free", "rgc_py_hash_node", "rgc_py_set_order", "rgc_test_epilogue",
            "rgc_score_pairs", "rgc_ilp_solve", "rgc_write_outputs", "rgc_pickle_bytes",
            "rgc_py_float_repr"]
@@ -252,15 +253,23 @@ class Context:
         self._pending = None
         self._lease = None   # weakref to the _HostLease of the last Result
 
+    def set_copy_stream(self, stream: int):
+        """Stream of the per-micrograph stats copy of non-lazy submits (0: the null stream);
+        by default all contexts share one copy stream per device (rgc_ctx_set_copy_stream)."""
+        _check(lib.rgc_ctx_set_copy_stream(self._p, C.c_void_p(stream or 0)))
+
     def _retire(self):
         """Before anything that may reuse or free the context's host buffers: if the last
         Result (or any array taken from it) is still referenced, hand its buffers over to it."""
-        ref, self._lease = self._lease, None
+        ref = self._lease
         lease = ref() if ref is not None else None
         if lease is not None and lease.block is None and self._p:
             h = C.c_void_p()
+            # (the lease is dropped only once the hand-over succeeded: after a failed detach
+            # the next retire, or close(), tries again)
             _check(lib.rgc_detach_host(self._p, C.byref(h)))
             lease.block = h.value
+        self._lease = None
 
     def _result(self, bo, n_mg, k, flags, lazy_ctx=None):
         lease = _HostLease()

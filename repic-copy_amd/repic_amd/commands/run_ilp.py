@@ -15,8 +15,11 @@ conflict components of up to 4096 cliques optimal exactly (f32 weights summed in
 picks, among equally good packings, the one its heaviest-first branch order meets first
 (Gurobi's choice among ties is unspecified).  Larger components, and components that exceed
 ``--node_limit``, get a greedy + swap local-search packing (or the branch and bound's best)
-certified by a Lagrangian dual bound: within Gurobi's default 1e-4 gap it is accepted silently,
-as Gurobi would; otherwise a warning names the micrograph and says which case it is.  Lines
+certified by a Lagrangian dual bound; the columns that bound leaves within its gap (reduced-
+cost fixing) are then searched exactly, which proves most of them optimal.  What remains
+within Gurobi's default 1e-4 gap is accepted silently, as Gurobi would; otherwise a warning
+names the micrograph and says which case it is.  The search is bounded by node counts only,
+so two runs give the same packings.  Lines
 of equal confidence follow our clique column order (the reference's is CPython set order,
 not reproducible, get_cliques.py:161).  With ``--multi_out`` inputs the
 reference raises AttributeError (``confidences`` is a tuple there, :97-106); so does this.
@@ -51,10 +54,9 @@ def add_arguments(parser):
     parser.add_argument("--num_particles", type=int,
                         help="filter for the number of expected particles (int)")
     parser.add_argument("--node_limit", type=int, default=0,
-                        help="branch-and-bound nodes per conflict component (0: 2^22)")
-    parser.add_argument("--time_limit", type=float, default=ilp.DEFAULT_TIME_LIMIT_S,
-                        help="seconds the branch and bound may search (<= 0: no limit; "
-                             "unfinished components are certified by their Lagrangian bound)")
+                        help="branch-and-bound nodes per conflict component (0: the library "
+                             "default, 2^14, x4 per reduced-cost-fixing pass); the only limit of the search, so the output does "
+                             "not depend on the device's speed or load")
     parser.add_argument("--device", type=int, default=None,
                         help="HIP device (default: $LOCAL_RANK or 0)")
 
@@ -88,9 +90,7 @@ def main(args):
         ctx = _lib.Context(dev)
         try:
             xs, status, rgap = solve_batch(ctx, mats, weights, getattr(args, "node_limit", 0),
-                                           statuses=True, gaps=True,
-                                           time_limit=getattr(args, "time_limit",
-                                                              ilp.DEFAULT_TIME_LIMIT_S))
+                                           statuses=True, gaps=True)
         finally:
             ctx.close()
     share = (time.time() - t0) / max(1, len(mats))

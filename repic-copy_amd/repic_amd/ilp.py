@@ -40,10 +40,6 @@ def pack(mats):
     return col_ptr, row_idx, row0, np.asarray(col_off, np.int64)
 
 
-# default time budget of the branch-and-bound search (rgc_ilp_in.time_limit_s, ABI 8): a
-# whole crowded C5 micrograph's medium components otherwise search for tens of seconds
-DEFAULT_TIME_LIMIT_S = 5.0
-
 # component statuses (include/repic_gc.h RGC_ILP_*)
 NODE_LIMIT, OPTIMAL, GAP_OK, HEURISTIC = 0, 1, 2, 3
 
@@ -64,13 +60,13 @@ def mg_status(ex, gap=0.0, primal=0.0):
     return GAP_OK
 
 
-def solve_batch(ctx, mats, weights, node_limit=0, timing=False, statuses=False, gaps=False,
-                time_limit=DEFAULT_TIME_LIMIT_S):
+def solve_batch(ctx, mats, weights, node_limit=0, timing=False, statuses=False, gaps=False):
     """Returns (x list of uint8 arrays, exact list of bool): per micrograph the chosen
     columns and whether every component was proven optimal (with ``statuses``: the
     micrograph status codes, mg_status, instead of the bools; with ``gaps`` also the
-    micrograph's relative gap bound, sum of component gaps / objective).  ``time_limit``
-    bounds the branch-and-bound search in seconds (None / <= 0: none)."""
+    micrograph's relative gap bound, sum of component gaps / objective).  The search is
+    bounded by ``node_limit`` nodes per component (0: the library default) and nothing else,
+    so the result is the same on every run and device."""
     col_ptr, row_idx, n_rows, col_off = pack(mats)
     w = np.ascontiguousarray(np.concatenate([np.asarray(v, np.float64).ravel() for v in weights])
                              if weights else np.zeros(0), dtype=np.float64)
@@ -83,7 +79,7 @@ def solve_batch(ctx, mats, weights, node_limit=0, timing=False, statuses=False, 
     gp = np.zeros(nc, np.float64)
     si = IlpIn(nc, n_rows, col_ptr.ctypes.data, row_idx.ctypes.data, w.ctypes.data,
                int(node_limit), _lib.F_TIMING if timing else 0, gp.ctypes.data,
-               float(time_limit or 0.0))
+               0.0)   # (time_limit_s: ignored since ABI 9)
     ctx._retire()   # a live Result of an earlier run keeps its host buffers
     _lib._check(_lib.lib.rgc_ilp_solve(ctx._p, C.byref(si), x.ctypes.data, ex.ctypes.data))
     xs = [x[col_off[m]:col_off[m + 1]] for m in range(len(mats))]

@@ -106,3 +106,51 @@ def test_pipelined_steps_order_and_depth(depth, n):
         assert 0 <= in_flight <= depth
     assert in_flight == 0
     assert kt.get("__steps", 0) == len(range(0, n, bench.TIME_EVERY))
+
+
+@pytest.mark.parametrize("total,world", [(100000, 1), (100000, 2), (100000, 3), (100000, 8),
+                                         (7, 8), (12, 5)])
+def test_fixed_shard_splits_one_batch(total, world):
+    """C4_100k_fixed (strong scaling): the ranks' shares of the fixed batch are contiguous,
+    cover it exactly once and differ by at most one micrograph."""
+    shares = [bench.fixed_shard(total, world, r) for r in range(world)]
+    assert shares[0][0] == 0
+    for (s0, n0), (s1, _) in zip(shares, shares[1:]):
+        assert s0 + n0 == s1
+    assert sum(n for _, n in shares) == total
+    assert max(n for _, n in shares) - min(n for _, n in shares) <= 1
+
+
+def test_stream_plan_fits_the_hardware_queues():
+    """bench.py's streams fit GPU_MAX_HW_QUEUES (4): the default depth's launch streams plus
+    the null stream (which also carries the non-lazy stats copies), no separate copy stream."""
+    plan = bench.stream_plan(bench.PIPE_DEPTH_DEFAULT)
+    assert plan["total"] <= bench.HW_QUEUES == 4
+    assert plan["copy_streams"] == 0 and plan["launch_streams"] == bench.PIPE_DEPTH_DEFAULT
+    with pytest.raises(AssertionError):
+        bench.stream_plan(bench.HW_QUEUES)
+
+
+def test_pmc_record_is_keyed_by_entry(tmp_path, monkeypatch):
+    """Counters are looked up by by_config ENTRY: a record taken at C4's bench size (no
+    "entry" key) stands for C4, never for C4_100k or C4_100k_fixed (other batch sizes)."""
+    import hashlib
+    import json
+    lib = tmp_path / "lib.so"
+    lib.write_bytes(b"x")
+    sha = hashlib.sha256(b"x").hexdigest()
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    (prof / "a_c4_traffic.json").write_text(json.dumps({"lib_sha256": sha, "config": "C4"}))
+    (prof / "b_c4_100k_traffic.json").write_text(json.dumps(
+        {"lib_sha256": sha, "config": "C4", "entry": "C4_100k"}))
+    (prof / "c_c2_traffic.json").write_text(json.dumps({"lib_sha256": sha}))
+    sys.path.insert(0, os.path.join(ROOT, "repic-copy_amd"))
+    from repic_amd import _lib
+    monkeypatch.setattr(_lib, "LIB_PATH", str(lib))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.pmc_record("C4")[1] == "a_c4_traffic.json"
+    assert bench.pmc_record("C4_100k")[1] == "b_c4_100k_traffic.json"
+    assert bench.pmc_record("C4_100k_fixed") == (None, None)
+    assert bench.pmc_record("C2")[1] == "c_c2_traffic.json"
+    assert bench.pmc_record("C5_256") == (None, None)

@@ -228,3 +228,23 @@ def test_bench_two_ranks_one_gpu():
     assert two["n_gpus"] == 2 and two["value"] > 0 and two["scaling"] == "weak"
     assert two["totals"] == one["totals"]
     assert two["totals"]["micrographs"] == 120
+
+
+@pytest.mark.gpu
+def test_bench_fixed_batch_two_ranks():
+    """The strong-scaling entry: `bench.py --gpus 2 --by-config C4_100k_fixed` (two
+    self-spawned ranks on cuda:0 over gloo) splits ONE 100k-micrograph C4 batch 50k / 50k and
+    reports its total of 100k micrographs per step, scaling "strong"."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(RGC_BENCH_DEVICE="0", RGC_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--config", "C2", "--n_mg", "20", "--by-config", "C4_100k_fixed",
+                        "--steps", "2", "--warmup", "1", "--no-cpu-baseline"], env=env,
+                       capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(s) for s in r.stdout.strip().splitlines() if s.startswith("{")]
+    assert len(lines) == 1
+    e = lines[0]["by_config"]["C4_100k_fixed"]
+    assert e["totals"]["micrographs"] == 100000 and e["micrographs_per_step"] == 100000
+    assert e["scaling"] == "strong" and e["micrographs_per_gpu"] == 50000 and e["value"] > 0

@@ -32,7 +32,7 @@ pass grbm GRBM_GUI_ACTIVE GRBM_COUNT
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE
 python3 tools/pmc_traffic.py "$OUT/fetch.csv" "$OUT/write.csv" repic-copy_amd/repic_amd/librepic_gc.so "$OUT/traffic.json" "$CFG"
-REPIC_GC_LIB=repic-copy_amd/repic_amd/librepic_gc_diag.so timeout -k 10 200 \
+REPIC_GC_LIB=abl/librepic_gc_diag.so timeout -k 10 200 \
   python -u tools/phase_stamps.py "$CFG" "$NMG" > "$OUT/stamps.txt" 2>&1 || { tail -20 "$OUT/stamps.txt"; exit 1; }
 cat "$OUT/stamps.txt"
 echo "== done"

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-phase cycle shares of the fused kernel from the diagnostic build (RGC_STAMPS).
 
-  REPIC_GC_LIB=repic-copy_amd/repic_amd/librepic_gc_diag.so python tools/phase_stamps.py [C2] [n_mg]
+  REPIC_GC_LIB=abl/librepic_gc_diag.so python tools/phase_stamps.py [C2] [n_mg]
 
 Prints, per phase, mean / p50 / p99 s_memtime cycles per workgroup, and the workgroup
 timeline (first start, last end) to see how many occupancy rounds the launch took.
@@ -13,7 +13,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "repic-copy_amd"))
-os.environ.setdefault("REPIC_GC_LIB", os.path.join(ROOT, "repic-copy_amd/repic_amd/librepic_gc_diag.so"))
+os.environ.setdefault("REPIC_GC_LIB", os.path.join(ROOT, "abl/librepic_gc_diag.so"))
 
 import numpy as np  # noqa: E402
 
