@@ -1799,7 +1799,7 @@ static int ilp_core(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact
 
 // The device solver, then (depth < ILP_FIX_DEPTH) reduced-cost fixing of the components it
 // left unproven, solved by the same function one level down.
-constexpr int ILP_FIX_DEPTH = 3;
+constexpr int ILP_FIX_DEPTH = 4;
 
 static int ilp_solve_rec(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* exact,
                          double* gap, int depth) {
@@ -1847,8 +1847,10 @@ static int ilp_solve_rec(rgc_ctx* c, const rgc_ilp_in* in, uint8_t* x, uint8_t* 
       sub.col_ptr = sub_ptr.data();
       sub.row_idx = sub_row.data();
       sub.w = sub_w.data();
-      // (4x the nodes one level down: its components are the few hard ones, restricted)
-      sub.node_limit = 4 * (in->node_limit > 0 ? in->node_limit : (int64_t)RGC_ILP_DEFAULT_NODES);
+      // (4x the nodes one level down, up to 16x the first pass's: its components are the few
+      // hard ones, restricted)
+      const int64_t nl = in->node_limit > 0 ? in->node_limit : (int64_t)RGC_ILP_DEFAULT_NODES;
+      sub.node_limit = depth < 2 ? 4 * nl : nl;
       std::vector<uint8_t> sx(sub_nc), sex(sub_nc);
       std::vector<double> sgap(sub_nc);
       // (with RGC_F_TIMING the second pass's sections follow "k_ilp_fixsearch" in the list)
