@@ -74,7 +74,7 @@ enum DevBufId {
   D_IL_RPTR, D_IL_RCOLS, D_IL_CID, D_IL_CN, D_IL_COFF, D_IL_CCUR, D_IL_MEM, D_IL_LOC, D_IL_SCR,
   D_IL_BIG, D_IL_NBIG, D_IL_WSCR, D_IL_X, D_IL_EX, D_IL_RLOC, D_IL_CERT, D_IL_KEY, D_IL_ST,
   D_IL_RMAX, D_IL_OWN, D_IL_LAM, D_IL_GRAD, D_IL_CS, D_IL_CNT, D_IL_GAP, D_IL_STSAVE,
-  D_IL_FS, D_IL_FSCNT, D_IL_FSKEEP,
+  D_IL_FS, D_IL_FSCNT, D_IL_FSKEEP, D_LBUCKET,
   D_COUNT
 };
 enum HostBufId {
@@ -91,7 +91,11 @@ struct Buf {
 // tools/probe/lds_occ.hip: 3 workgroups per CU up to 53760 B, 2 above it; the HIP occupancy
 // API over-reports 3 up to 54613 B, so it is not used).
 constexpr int LDS_BLOCK = 1280;
+#ifdef RGC_STAMPS
+constexpr int LDS_BLOCKS = 127;   // (diagnostic build: the fused kernel's static LDS counters)
+#else
 constexpr int LDS_BLOCKS = 128;
+#endif
 // Micrographs above this many boxes go straight to the large-micrograph route.  Above 2048
 // boxes the fused layout uses 2 n grid cells and u16 parents (29 B per box + 2 B per edge),
 // so a 4096-box micrograph (C3: ~4k boxes, ~15k edges) runs in one workgroup per CU with room
@@ -388,7 +392,7 @@ static int fused_io(rgc_ctx* c, int n_mg, size_t cur_off, FusedIo* io) {
 // Runs the multi-kernel pipeline on a (sub-)batch whose x/y/score are device arrays, writing
 // per-clique outputs at [out_base, out_base + C).  Fills st_out[n_mg] (clique_base/cnt set).
 static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int get_cc, int multi,
-                     bool want_ji, const int64_t* box_off, const int64_t* id_base, const double* x,
+                     bool want_members, bool want_ji, const int64_t* box_off, const int64_t* id_base, const double* x,
                      const double* y, const double* sc, int64_t out_base,
                      std::vector<MgStat>& st_out, int64_t* C_out, int64_t* E_out) {
   const int64_t N = box_off[(int64_t)n_mg * k];
@@ -617,8 +621,13 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   A.conf = D<float>(c, D_CONF) + out_base;
   A.consensus = D<int32_t>(c, D_CONS) + out_base;
   A.order = multi ? D<uint8_t>(c, D_ORDER) + out_base * k : nullptr;
-  TRY(mark(c, "k5_leaf_fill"));
-  launch_clique_level(s, k == 2, true, true, A, L);
+  // k >= 3 without members in the outputs: the leaf level's cliques are generated inside their
+  // epilogue (k5_leaf_epi), their members never written (the exact pass's excepted)
+  const bool leaf_epi = !want_members && !multi && k >= 3;
+  if (!leaf_epi) {
+    TRY(mark(c, "k5_leaf_fill"));
+    launch_clique_level(s, k == 2, true, true, A, L);
+  }
   TRY(mark(c, "k5_dfs_fill"));
   launch_cliques_dfs(s, true, (int)N, A);
   // exact list [C], ballot words [ceil(C / 64)], per compaction wave: offsets and counts
@@ -634,14 +643,27 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   A.excount = reinterpret_cast<unsigned long long*>(d_tot + 3);
   TRY(ensure_dev(c, D_PK, (size_t)N * 16));
   A.pk = D<double>(c, D_PK);
+  // the epilogues set one bit per clique for the exact pass in these words
+  HIPCHK(hipMemsetAsync(A.exmask, 0, exw * 8, s));
   TRY(mark(c, "k5_pack"));
   launch_clique_pack(s, (int)N, A);
+  A.epi_lo = 0;
+  if (leaf_epi) {
+    TRY(mark(c, "k5_leaf_epi"));
+    // (the prefix holding each wave's first clique)
+    TRY(ensure_dev(c, D_LBUCKET, ((C1 + 127) / 128 + 1) * 4));
+    if (launch_clique_leaf_epi(s, A, L, D<int32_t>(c, D_LBUCKET), C1) != 0)
+      return fail("unsupported k");
+    A.epi_lo = C1;   // k5_epilogue: the DFS route's cliques only
+  }
   TRY(mark(c, "k5_epilogue"));
   launch_clique_epilogue(s, false, A);
   TRY(mark(c, "k5_epi_exact"));
   launch_clique_epilogue(s, true, A);
   TRY(mark(c, "k5_ranges"));
-  launch_clique_ranges(s, A, C1, D<int64_t>(c, D_RLO), D<int64_t>(c, D_RLO) + n_mg);
+  launch_clique_ranges(s, A, C1, D<int64_t>(c, D_RLO), D<int64_t>(c, D_RLO) + n_mg,
+                       leaf_epi ? L.in_root : nullptr, leaf_epi ? L.off : nullptr,
+                       leaf_epi ? L.n_items : 0);
   HIPCHK(hipMemcpyAsync(H<void>(c, H_STAT), D<void>(c, D_STAT), n_mg * sizeof(MgStat),
                         hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(H<void>(c, H_MGOFF), D<void>(c, D_RLO), 2 * (size_t)n_mg * 8,
@@ -820,8 +842,8 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
       A.esum_n = 0;   // (the host sums the finished micrographs' edges from the stats copy)
       int64_t ties_done = 0;   // entries of earlier passes already resolved
 #ifdef RGC_STAMPS
-      TRY(ensure_dev(c, D_STAMPS, 3 * (size_t)n_mg * 16 * 8));
-      HIPCHK(hipMemsetAsync(D<void>(c, D_STAMPS), 0, 3 * (size_t)n_mg * 128, s));
+      TRY(ensure_dev(c, D_STAMPS, 3 * (size_t)n_mg * rgc::STAMP_SLOTS * 8));
+      HIPCHK(hipMemsetAsync(D<void>(c, D_STAMPS), 0, 3 * (size_t)n_mg * rgc::STAMP_SLOTS * 8, s));
 #endif
       std::vector<int32_t> todo = todo0, left;
       int ml_off = 0;   // mg-list slots used (earlier passes' lists stay intact)
@@ -869,7 +891,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
           A.ecap = pl.ecap;
           A.mg_list = single ? nullptr : D<int32_t>(c, D_MGLIST) + ml_off + starts[q];
 #ifdef RGC_STAMPS
-          A.stamps = D<unsigned long long>(c, D_STAMPS) + (size_t)(ml_off + starts[q]) * 16;
+          A.stamps = D<unsigned long long>(c, D_STAMPS) + (size_t)(ml_off + starts[q]) * rgc::STAMP_SLOTS;
 #endif
           TRY(ensure_qg(c, A, k, pl.nt));
           TRY(mark(c, "k_fused"));
@@ -915,8 +937,9 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
       c->cur_slot = 1 - c->cur_slot;
 #ifdef RGC_STAMPS
       const size_t n0w = all0 ? (size_t)n_mg : todo0.size();   // pass 0's workgroups
-      c->stamps.resize(n0w * 16);
-      HIPCHK(hipMemcpy(c->stamps.data(), D<void>(c, D_STAMPS), n0w * 128, hipMemcpyDeviceToHost));
+      c->stamps.resize(n0w * rgc::STAMP_SLOTS);
+      HIPCHK(hipMemcpy(c->stamps.data(), D<void>(c, D_STAMPS), n0w * rgc::STAMP_SLOTS * 8,
+                       hipMemcpyDeviceToHost));
 #endif
       fused_edges = (int64_t)h_cur[2];
       const bool edge_over = want_edges && fused_edges > c->cap_edges;
@@ -986,12 +1009,12 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
     }
     std::vector<MgStat> sst;
     int64_t Cm = 0, Em = 0;
-    TRY(run_multi(c, ns, k, B, two_b2, get_cc, multi, want_edges, sbo.data(), sid.data(), sx, sy, ss,
-                  fused_total, sst, &Cm, &Em));
+    TRY(run_multi(c, ns, k, B, two_b2, get_cc, multi, want_members, want_edges, sbo.data(),
+                  sid.data(), sx, sy, ss, fused_total, sst, &Cm, &Em));
     if (!ident) {
       TRY(mark(c, "k_remap"));
       launch_remap(s, Cm, k, orig, D<int32_t>(c, D_CONS) + fused_total,
-                   D<int32_t>(c, D_MEMBERS) + fused_total * k);
+                   want_members ? D<int32_t>(c, D_MEMBERS) + fused_total * k : nullptr);
     }
     if (want_edges) {
       TRY(ensure_edges(c, fused_edges + Em, fused_edges));

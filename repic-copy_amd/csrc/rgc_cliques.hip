@@ -332,8 +332,11 @@ __global__ __launch_bounds__(WG) void k5_leaf_fill(CliqueArgs A, LevelArgs L) {
 // Per-micrograph clique range.  Level-route cliques [0, C1) are sorted by root (box index, so
 // by micrograph): binary search for the micrograph's first and last picker-0 box.  DFS-route
 // micrographs: their roots' scanned offsets after C1.
+// (leaf_root / leaf_off: the leaf prefixes' roots, nondecreasing, and clique offsets, when the
+// members were not written: the first clique of root g is leaf_off[lower_bound(leaf_root, g)])
 __global__ __launch_bounds__(WG) void k5_ranges(CliqueArgs A, int64_t C1, int64_t* rlo,
-                                               int64_t* rhi) {
+                                               int64_t* rhi, const int32_t* leaf_root,
+                                               const int64_t* leaf_off, int64_t n_leaf) {
   const int m = blockIdx.x * WG + threadIdx.x;
   if (m >= A.n_mg) return;
   const int g0 = A.box_off[m * A.k], g1 = A.box_off[m * A.k + 1];
@@ -346,12 +349,21 @@ __global__ __launch_bounds__(WG) void k5_ranges(CliqueArgs A, int64_t C1, int64_
   const int key[2] = {g0, g1};
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    int64_t a = 0, z = C1;
-    while (a < z) {
-      const int64_t mid = (a + z) >> 1;
-      if (A.members[mid * A.k] < key[t]) a = mid + 1; else z = mid;
+    if (leaf_root) {
+      int64_t a = 0, z = n_leaf;
+      while (a < z) {
+        const int64_t mid = (a + z) >> 1;
+        if (leaf_root[mid] < key[t]) a = mid + 1; else z = mid;
+      }
+      b[t] = leaf_off[a];
+    } else {
+      int64_t a = 0, z = C1;
+      while (a < z) {
+        const int64_t mid = (a + z) >> 1;
+        if (A.members[mid * A.k] < key[t]) a = mid + 1; else z = mid;
+      }
+      b[t] = a;
     }
-    b[t] = a;
   }
   rlo[m] = b[0];
   rhi[m] = b[1];
@@ -445,10 +457,8 @@ __global__ __launch_bounds__(WG) void k5_pack(int N, CliqueArgs A) {
 // Member gathers of one clique: COO rows (vertex ranks by (x, y, id), ascending) stored,
 // conf = f32(median score), the packed coordinates for the overlap paths.
 template <int K>
-__device__ __forceinline__ void epi_gather(const CliqueArgs& A, int64_t j, int (&mem)[K],
-                                           uint32_t (&xy)[K], float* conf32) {
-#pragma unroll
-  for (int i = 0; i < K; ++i) mem[i] = A.members[j * K + i];
+__device__ __forceinline__ void epi_gather_mem(const CliqueArgs& A, int64_t j, const int (&mem)[K],
+                                               uint32_t (&xy)[K], float* conf32) {
   double s[K];
   int r[K];
 #pragma unroll
@@ -463,6 +473,13 @@ __device__ __forceinline__ void epi_gather(const CliqueArgs& A, int64_t j, int (
 #pragma unroll
   for (int i = 0; i < K; ++i) A.rows[j * K + i] = r[i];
   *conf32 = (float)median_n<K>(s);   // conf = f32(median score)
+}
+template <int K>
+__device__ __forceinline__ void epi_gather(const CliqueArgs& A, int64_t j, int (&mem)[K],
+                                           uint32_t (&xy)[K], float* conf32) {
+#pragma unroll
+  for (int i = 0; i < K; ++i) mem[i] = A.members[j * K + i];
+  epi_gather_mem<K>(A, j, mem, xy, conf32);
 }
 
 // One clique's weighted-degree candidate and median JI: exact floats for integer coordinates
@@ -589,16 +606,18 @@ __device__ __forceinline__ uint64_t spread_even(uint64_t v) {
 #define RGC_EPI_WPE_N 3
 #endif
 #define RGC_EPI_WPE __attribute__((amdgpu_waves_per_eu(RGC_EPI_WPE_N)))
+// The epilogue of cliques j0 and j1 (j1 only with ``two``) whose members are known: rows and
+// conf (epi_gather_mem), then w and the consensus; cliques that need the exact f64 pass get
+// their bit in exmask (zeroed before the launch; bit j & 63 of word j >> 6) and, with
+// ``keep_members``, their members for that pass.
 template <int K>
-__global__ __launch_bounds__(WG) RGC_EPI_WPE void k5_epilogue(CliqueArgs A) {
-  const int64_t j0 = 2 * ((int64_t)blockIdx.x * WG + threadIdx.x);
-  if (j0 >= A.C) return;
-  const bool two = j0 + 1 < A.C;
-  int mem0[K], mem1[K];
+__device__ __forceinline__ void epi_two(const CliqueArgs& A, int64_t j0, int64_t j1, bool two,
+                                        const int (&mem0)[K], const int (&mem1)[K],
+                                        bool keep_members) {
   uint32_t xy0[K], xy1[K];
   float cf0, cf1 = 0.0f;
-  epi_gather<K>(A, j0, mem0, xy0, &cf0);
-  if (two) epi_gather<K>(A, j0 + 1, mem1, xy1, &cf1);
+  epi_gather_mem<K>(A, j0, mem0, xy0, &cf0);
+  if (two) epi_gather_mem<K>(A, j1, mem1, xy1, &cf1);
   const double B = A.B;
   const bool multi = (A.flags & 2) != 0;
   bool ex[2] = {multi, multi};
@@ -616,31 +635,152 @@ __global__ __launch_bounds__(WG) RGC_EPI_WPE void k5_epilogue(CliqueArgs A) {
   A.w[j0] = (float)((double)cf0 * med[0]);
   A.conf[j0] = cf0;
   if (two) {
-    A.w[j0 + 1] = (float)((double)cf1 * med[1]);
-    A.conf[j0 + 1] = cf1;
+    A.w[j1] = (float)((double)cf1 * med[1]);
+    A.conf[j1] = cf1;
   }
-  // the cliques that need exact f64 degrees / node order (~3 % on C5, i.e. most waves hold
-  // one): k5_ex_compact + k5_epi_exact, their 64-bit hashing and K x K JIs out of this
-  // kernel's register budget.  Ballot words, bit j & 63 of word j >> 6: this wave's 128
-  // cliques are words 2w (lanes 0-31) and 2w + 1 (lanes 32-63), no global atomics.
-  const uint64_t b0 = __ballot(ex[0]), b1 = __ballot(ex[1] && two);
-  if ((threadIdx.x & 63) == 0) {
-    A.exmask[j0 >> 6] = spread_even(b0) | (spread_even(b1) << 1);
-    if (j0 + 64 < A.C)
-      A.exmask[(j0 >> 6) + 1] = spread_even(b0 >> 32) | (spread_even(b1 >> 32) << 1);
-  }
-  if (!ex[0]) {
+  // the cliques that need exact f64 degrees / node order (~3 % on C5): k5_ex_wtot /
+  // k5_ex_write + k5_epi_exact, their 64-bit hashing and K x K JIs out of this kernel's
+  // register budget.  One non-returning atomic OR per such clique into the zeroed words.
+  if (ex[0]) {
+    atomicOr(reinterpret_cast<unsigned long long*>(A.exmask) + (j0 >> 6), 1ull << (j0 & 63));
+    if (keep_members)
+#pragma unroll
+      for (int i = 0; i < K; ++i) A.members[j0 * K + i] = mem0[i];
+  } else {
     int cons = mem0[0];
 #pragma unroll
     for (int i = 1; i < K; ++i) cons = (arg[0] == i) ? mem0[i] : cons;
     A.consensus[j0] = cons;
   }
-  if (two && !ex[1]) {
-    int cons = mem1[0];
+  if (two) {
+    if (ex[1]) {
+      atomicOr(reinterpret_cast<unsigned long long*>(A.exmask) + (j1 >> 6), 1ull << (j1 & 63));
+      if (keep_members)
 #pragma unroll
-    for (int i = 1; i < K; ++i) cons = (arg[1] == i) ? mem1[i] : cons;
-    A.consensus[j0 + 1] = cons;
+        for (int i = 0; i < K; ++i) A.members[j1 * K + i] = mem1[i];
+    } else {
+      int cons = mem1[0];
+#pragma unroll
+      for (int i = 1; i < K; ++i) cons = (arg[1] == i) ? mem1[i] : cons;
+      A.consensus[j1] = cons;
+    }
   }
+}
+
+// Thread t takes cliques epi_lo + 2t and epi_lo + 2t + 1 (members from A.members).
+template <int K>
+__global__ __launch_bounds__(WG) RGC_EPI_WPE void k5_epilogue(CliqueArgs A) {
+  const int64_t j0 = A.epi_lo + 2 * ((int64_t)blockIdx.x * WG + threadIdx.x);
+  if (j0 >= A.C) return;
+  const bool two = j0 + 1 < A.C;
+  int mem0[K], mem1[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) mem0[i] = A.members[j0 * K + i];
+  if (two)
+#pragma unroll
+    for (int i = 0; i < K; ++i) mem1[i] = A.members[(j0 + 1) * K + i];
+  epi_two<K>(A, j0, j0 + 1, two, mem0, mem1, false);
+}
+
+// The level route's leaf level and the epilogue in one pass (k >= 3, outputs without
+// members).  Wave w takes cliques [128 w, 128 w + 128) of the level route (the old epilogue's
+// balance: two per lane); every leaf prefix holds 1..64 cliques (a prefix is kept only when it
+// has a leaf), so those cliques come from at most 128 consecutive prefixes, starting at the one
+// k5_leaf_bucket recorded for the wave.  The prefixes' offsets, leaf masks, forward-list starts
+// and members are staged in LDS; lane l derives the members of cliques l and l + 64 (binary
+// search over the staged offsets, the rank-th set bit of the leaf mask, the leaf's box from
+// the root's forward list) and runs the epilogue on them.  The members never go to HBM (except
+// those of the ~3 % of cliques the exact pass takes): k5_leaf_fill wrote C K ints that
+// k5_epilogue read back (4 GB of traffic per C5 step of 64 micrographs).
+constexpr int LE_Q = 128;   // cliques per wave
+
+// position of the t-th (0-based) set bit of m (t < popcount(m)): six halving steps
+__device__ __forceinline__ int select_bit(uint64_t m, int t) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const int c = __popcll(m & ((1ull << w) - 1));
+    if (t >= c) {
+      t -= c;
+      m >>= w;
+      pos += w;
+    }
+  }
+  return pos;
+}
+
+// bucket[b] = the leaf prefix that holds clique LE_Q b (at most one bucket start per prefix)
+__global__ __launch_bounds__(WG) void k5_leaf_bucket(LevelArgs L, int32_t* bucket) {
+  const int64_t i = (int64_t)blockIdx.x * WG + threadIdx.x;
+  if (i >= L.n_items) return;
+  const int64_t lo = L.off[i], hi = L.off[i + 1];
+  for (int64_t b = (lo + LE_Q - 1) / LE_Q; b * LE_Q < hi; ++b) bucket[b] = (int32_t)i;
+}
+
+// (k = 8 spills 64 bytes per lane at 3 waves per SIMD; at 2 waves per SIMD, no spill, it ran
+// 15 % slower: profiles/r06l_*)
+template <int K>
+__global__ __launch_bounds__(WG) RGC_EPI_WPE void k5_leaf_epi(CliqueArgs A, LevelArgs L,
+                                                           const int32_t* bucket, int64_t C1) {
+  constexpr int NWV = WG / 64;
+  constexpr int NM = K - 1;                  // staged members: the root and pickers 1..K-2
+  __shared__ int32_t s_off[NWV][LE_Q];       // prefix's first clique - the wave's first
+  __shared__ uint64_t s_c[NWV][LE_Q];        // leaf masks
+  __shared__ int64_t s_lo[NWV][LE_Q];        // root's forward-list start
+  __shared__ int32_t s_m[NWV][NM][LE_Q];     // the prefix's members (the same for its cliques)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t w = (int64_t)blockIdx.x * NWV + wv;
+  const int64_t j0 = w * LE_Q;
+  if (j0 >= C1) return;   // wave-uniform
+  const int64_t a0 = bucket[w];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int t = lane + 64 * h;
+    const int64_t i = a0 + t;
+    int32_t o = INT_MAX;
+    uint64_t c = 0;
+    int64_t lo = 0;
+    if (i < L.n_items) {
+      const int64_t oi = L.off[i] - j0;
+      if (oi < LE_Q) {   // (prefixes past the wave's range stay unstaged)
+        o = (int32_t)oi;
+        const int r = L.in_root[i];
+        const uint64_t P = L.in_P[i];
+        lo = A.fwd_off[r];
+        c = L.in_M[i] & picker_lanes(A.rbound[r], L.D + 1);
+        s_m[wv][0][t] = r;
+#pragma unroll
+        for (int u = 0; u < K - 2; ++u) s_m[wv][u + 1][t] = A.e_dst[lo + ((P >> (6 * u)) & 63)];
+      }
+    }
+    s_off[wv][t] = o;
+    s_c[wv][t] = c;
+    s_lo[wv][t] = lo;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  auto members_of = [&](int q, int (&mem)[K]) {
+    // the last staged prefix whose first clique is <= q (s_off[0] <= 0)
+    int a = 0;
+#pragma unroll
+    for (int step = 64; step >= 1; step >>= 1)
+      if (a + step < LE_Q && s_off[wv][a + step] <= q) a += step;
+    const int v = select_bit(s_c[wv][a], q - s_off[wv][a]);   // the leaf's lane
+#pragma unroll
+    for (int t = 0; t < NM; ++t) mem[t] = s_m[wv][t][a];
+    mem[K - 1] = A.e_dst[s_lo[wv][a] + v];
+  };
+  const int qa = lane, qb = lane + 64;
+  if (j0 + qa >= C1) return;
+  const bool two = j0 + qb < C1;
+  int mem0[K], mem1[K];
+  members_of(qa, mem0);
+  if (two) members_of(qb, mem1);
+  else
+#pragma unroll
+    for (int t = 0; t < K; ++t) mem1[t] = mem0[t];
+  epi_two<K>(A, j0 + qa, j0 + qb, two, mem0, mem1, true);
 }
 
 // The deferred cliques as a list: one wave per 64 ballot words (4096 cliques) ranks their set
@@ -788,12 +928,14 @@ static void ex_compact(hipStream_t stream, const CliqueArgs& A, int64_t nb) {
 int launch_clique_epilogue(hipStream_t stream, bool exact_pass, const CliqueArgs& A) {
   const int64_t nb = (A.C + WG - 1) / WG;
   if (nb <= 0) return 0;
+  const int64_t nbe = (A.C - A.epi_lo + WG - 1) / WG;   // k5_epilogue: [epi_lo, C)
   switch (A.k) {
 #define RGC_EPI(KK)                                                                      \
   case KK:                                                                               \
-    if (!exact_pass)                                                                     \
-      hipLaunchKernelGGL((k5_epilogue<KK>), dim3((nb + 1) / 2), dim3(WG), 0, stream, A); \
-    else {                                                                               \
+    if (!exact_pass) {                                                                   \
+      if (nbe > 0)                                                                       \
+        hipLaunchKernelGGL((k5_epilogue<KK>), dim3((nbe + 1) / 2), dim3(WG), 0, stream, A); \
+    } else {                                                                             \
       ex_compact(stream, A, nb);                                                         \
       hipLaunchKernelGGL((k5_epi_exact<KK>), dim3(std::min<int64_t>(nb, RGC_EXGRID)),      \
                          dim3(WG), 0, stream, A);                                        \
@@ -806,15 +948,34 @@ int launch_clique_epilogue(hipStream_t stream, bool exact_pass, const CliqueArgs
   return 0;
 }
 
+int launch_clique_leaf_epi(hipStream_t stream, const CliqueArgs& A, const LevelArgs& L,
+                           int32_t* bucket, int64_t C1) {
+  const int64_t nb = (L.n_items + WG - 1) / WG;
+  if (nb <= 0 || C1 <= 0) return 0;
+  hipLaunchKernelGGL(k5_leaf_bucket, dim3(nb), dim3(WG), 0, stream, L, bucket);
+  const int64_t nw = (C1 + LE_Q - 1) / LE_Q, nbe = (nw + WG / 64 - 1) / (WG / 64);
+  switch (A.k) {
+#define RGC_LE(KK) \
+  case KK:         \
+    hipLaunchKernelGGL((k5_leaf_epi<KK>), dim3(nbe), dim3(WG), 0, stream, A, L, bucket, C1); \
+    break;
+    RGC_LE(3) RGC_LE(4) RGC_LE(5) RGC_LE(6) RGC_LE(7) RGC_LE(8)
+#undef RGC_LE
+    default: return -1;
+  }
+  return 0;
+}
+
 void launch_clique_pack(hipStream_t stream, int N, const CliqueArgs& A) {
   if (N > 0) hipLaunchKernelGGL(k5_pack, dim3((N + WG - 1) / WG), dim3(WG), 0, stream, N, A);
 }
 
 void launch_clique_ranges(hipStream_t stream, const CliqueArgs& A, int64_t C1, int64_t* rlo,
-                          int64_t* rhi) {
+                          int64_t* rhi, const int32_t* leaf_root, const int64_t* leaf_off,
+                          int64_t n_leaf) {
   if (A.n_mg > 0)
     hipLaunchKernelGGL(k5_ranges, dim3((A.n_mg + WG - 1) / WG), dim3(WG), 0, stream, A, C1, rlo,
-                       rhi);
+                       rhi, leaf_root, leaf_off, n_leaf);
 }
 
 }  // namespace rgc

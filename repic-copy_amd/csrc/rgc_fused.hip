@@ -24,6 +24,28 @@
 
 #include <type_traits>
 
+#ifdef RGC_STAMPS
+// Diagnostic build only: every workgroup barrier of this file (and of the rgc_device.h scans
+// it inlines) adds the cycles each wave waits in it to that wave's counter, read and reset by
+// STAMP at each phase end, so a phase's barrier-wait share (waves idle behind the slowest
+// wave of the workgroup) separates from its other stalls.
+#include <hip/hip_runtime.h>
+namespace rgc {
+__shared__ unsigned long long g_bwait[16];
+__device__ __forceinline__ void raw_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+__device__ __forceinline__ void timed_barrier() {
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  raw_barrier();
+  if ((threadIdx.x & 63) == 0) g_bwait[threadIdx.x >> 6] += __builtin_amdgcn_s_memtime() - t0;
+}
+}  // namespace rgc
+#define __syncthreads() ::rgc::timed_barrier()
+#endif
+
 #include "rgc_device.h"
 #include "rgc_kernels.h"
 
@@ -1102,8 +1124,13 @@ void k_fused(FusedArgs A) {
   // diagnostic build only: per-phase s_memtime stamps of thread 0 (never in the product .so)
 #define STAMP(i)                                                                            \
   do {                                                                                      \
-    __syncthreads();                                                                        \
-    if (tid == 0) A.stamps[(int64_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime();   \
+    if ((tid & 63) == 0) {                                                                  \
+      A.stamps[(int64_t)blockIdx.x * STAMP_SLOTS + 16 + 16 * (i) + (tid >> 6)] =              \
+          (i) == 0 ? 0ull : g_bwait[tid >> 6];                                              \
+      g_bwait[tid >> 6] = 0;                                                                \
+    }                                                                                       \
+    raw_barrier();                                                                          \
+    if (tid == 0) A.stamps[(int64_t)blockIdx.x * STAMP_SLOTS + (i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
 #define STAMP(i) \
@@ -1676,8 +1703,8 @@ void k_fused(FusedArgs A) {
   STAMP(8);   // cliques
 #ifdef RGC_STAMPS
   if (tid == 0) {   // diagnostic build: root chunks of the BFS (0 = DFS fallback) and cliques
-    A.stamps[(int64_t)blockIdx.x * 16 + 14] = (unsigned long long)nch;
-    A.stamps[(int64_t)blockIdx.x * 16 + 15] = (unsigned long long)C;
+    A.stamps[(int64_t)blockIdx.x * STAMP_SLOTS + 14] = (unsigned long long)nch;
+    A.stamps[(int64_t)blockIdx.x * STAMP_SLOTS + 15] = (unsigned long long)C;
   }
 #endif
   // the output reservation: one returning atomic on the batch cursor per micrograph.  Its
@@ -1869,7 +1896,7 @@ void k_fused(FusedArgs A) {
   STAMP(12);
 #ifdef RGC_STAMPS
   if (tid == 0)
-    A.stamps[(int64_t)blockIdx.x * 16 + 13] =
+    A.stamps[(int64_t)blockIdx.x * STAMP_SLOTS + 13] =
         ((unsigned long long)(uint32_t)__builtin_amdgcn_s_memrealtime() << 32) | rt0;
 #endif
   if constexpr (QG) {
@@ -1950,8 +1977,13 @@ int launch_fused_ties(hipStream_t stream, const FusedArgs& A, int64_t from) {
 template <int K, bool W, int NT, bool QG = false>
 static int launch_fused_t(hipStream_t stream, int n_blocks, int lds_bytes, const FusedArgs& A) {
   static std::atomic<uint64_t> attr_set{0};   // per device
+#ifdef RGC_STAMPS
+  constexpr int kStaticLds = 256;   // (diagnostic build: g_bwait is static LDS)
+#else
+  constexpr int kStaticLds = 0;
+#endif
   const hipError_t e = set_dyn_lds_once(attr_set, reinterpret_cast<const void*>(&k_fused<K, W, NT, QG>),
-                                        160 * 1024);
+                                        160 * 1024 - kStaticLds);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL((k_fused<K, W, NT, QG>), dim3(n_blocks), dim3(NT), lds_bytes, stream, A);
   return (int)hipGetLastError();

@@ -89,6 +89,10 @@ inline MgOut mgout_bind(void* base, int n_mg) {
   return o;
 }
 
+// diagnostic build (RGC_STAMPS): per fused workgroup, 16 slots (phase releases by thread 0,
+// the workgroup timeline, chunk and clique counts), then each wave's arrival at each of the
+// 13 phase barriers (slot 16 + 16 * phase + wave)
+constexpr int STAMP_SLOTS = 16 + 13 * 16;
 struct FusedArgs {
   int k, flags;                 // flags: bit0 get_cc, bit1 multi_out, bit5 members
   double B, two_b2;
@@ -114,7 +118,7 @@ struct FusedArgs {
   int32_t* consensus;
   int32_t* members;
   uint8_t* order;
-  unsigned long long* stamps;   // diagnostic build (RGC_STAMPS) only: 8 stamps per WG
+  unsigned long long* stamps;   // diagnostic build (RGC_STAMPS) only: STAMP_SLOTS per WG
   // RGC_F_EDGES test hook (nullptr otherwise): every JI > 0.3 edge as (u, v, JI) with batch
   // box indices, reserved per micrograph on cursor[2]; nothing is written past ecap_out
   int32_t* eu;
@@ -192,6 +196,8 @@ struct CliqueArgs {
   int64_t* exwoff;            // [ceil(C / 4096) + 1] their scanned offsets
   int64_t* tiles;             // scan tile buffer (launch_scan)
   int64_t dfs_base;          // first output clique of the DFS route
+  int64_t epi_lo;            // first clique k5_epilogue handles (the level route's cliques
+                             // [0, dfs_base) may come from k5_leaf_epi instead)
   int32_t* members;
   int32_t* rows;
   float* w;
@@ -253,8 +259,12 @@ int launch_clique_level(hipStream_t stream, bool first, bool leaf, bool fill, co
                         const LevelArgs& L);
 int launch_clique_epilogue(hipStream_t stream, bool exact_pass, const CliqueArgs& A);
 void launch_clique_pack(hipStream_t stream, int N, const CliqueArgs& A);
+// (bucket: (C1 + 127) / 128 int32 of scratch)
+int launch_clique_leaf_epi(hipStream_t stream, const CliqueArgs& A, const LevelArgs& L,
+                           int32_t* bucket, int64_t C1);
 void launch_clique_ranges(hipStream_t stream, const CliqueArgs& A, int64_t C1, int64_t* rlo,
-                          int64_t* rhi);
+                          int64_t* rhi, const int32_t* leaf_root, const int64_t* leaf_off,
+                          int64_t n_leaf);
 int launch_cliques_dfs(hipStream_t stream, bool fill, int N, const CliqueArgs& A);
 void launch_rank(hipStream_t stream, int N, int n_mg, int k, const int32_t* box_off,
                  const int32_t* bmg, const MgGrid* grid, const double* x, const double* y,

@@ -826,7 +826,8 @@ __global__ __launch_bounds__(WG) void k_remap(int64_t C, int k, const int32_t* _
   const int64_t j = (int64_t)blockIdx.x * WG + threadIdx.x;
   if (j >= C) return;
   consensus[j] = orig[consensus[j]];
-  for (int i = 0; i < k; ++i) members[j * k + i] = orig[members[j * k + i]];
+  if (members)   // (only when members are outputs: otherwise most were never written)
+    for (int i = 0; i < k; ++i) members[j * k + i] = orig[members[j * k + i]];
 }
 
 // RGC_F_EDGES test hook: the sub-batch's edge list (u, v, JI) in batch box indices.

@@ -34,7 +34,8 @@ f.restype = C.c_int64
 n = f(ctx._p, None, 0)
 buf = (C.c_uint64 * n)()
 f(ctx._p, buf, n)
-raw = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 16).astype(np.int64)
+SLOTS = 16 + 13 * 16   # rgc_kernels.h STAMP_SLOTS
+raw = np.frombuffer(buf, dtype=np.uint64).reshape(-1, SLOTS).astype(np.int64)
 st = raw[:, :13]
 nch, ncl = raw[:, 14], raw[:, 15]
 print(f"BFS root chunks per micrograph: mean {nch.mean():.2f} p50 {np.median(nch):.0f} "
@@ -49,6 +50,27 @@ print(f"{cfg_name}: {n_mg} micrographs, {valid.sum()} complete WGs, cliques {r.n
 for i, nm in enumerate(names):
     print(f"  {nm:18s} mean {d[:, i].mean():9.0f}  p50 {np.median(d[:, i]):9.0f}  "
           f"p99 {np.percentile(d[:, i], 99):9.0f}  share {d[:, i].sum() / tot.sum():6.1%}")
+# barrier waits: slot 16 + 16 (i + 1) + w = cycles wave w waited in the workgroup barriers of
+# phase i (timed barriers of the diagnostic build).  Per phase: the mean wave's barrier-wait
+# share of the phase, and the spread of the waves' waits (max - min: the skew between the
+# first and last wave to arrive, summed over the phase's barriers)
+bw = raw[valid, 16:].reshape(-1, 13, 16)[:, 1:, :]
+nw = int(max(1, (bw.sum(axis=(0, 1)) > 0).sum()))
+bw = bw[:, :, :nw].astype(np.float64)
+print(f"  barrier waits ({nw} waves per workgroup): share of phase cycles, mean wave / "
+      f"skew (max - min wave) / phase")
+rows = []
+for i, nm in enumerate(names):
+    ph = d[:, i].astype(np.float64)
+    mean_w = bw[:, i, :].mean(axis=1)
+    skew = bw[:, i, :].max(axis=1) - bw[:, i, :].min(axis=1)
+    share = mean_w.sum() / max(ph.sum(), 1)
+    sk = skew.sum() / max(ph.sum(), 1)
+    rows.append((nm, d[:, i].sum() / tot.sum(), share, sk))
+    print(f"  {nm:18s} phase share {d[:, i].sum() / tot.sum():6.1%}  barrier-wait {share:6.1%}  "
+          f"skew {sk:6.1%}  (of the whole WG: {mean_w.sum() / tot.sum():6.1%})")
+allw = sum(bw[:, i, :].mean(axis=1).sum() for i in range(len(names)))
+print(f"  all phases: waves wait in barriers {allw / tot.sum():.1%} of the workgroup's cycles")
 print(f"  per-WG total cycles: mean {tot.mean():.0f} p50 {np.median(tot):.0f} p99 {np.percentile(tot, 99):.0f}")
 span = st[valid, 12].max() - st[valid, 0].min()
 print(f"  launch span {span} cycles; sum(WG cycles)/span = {tot.sum() / span:.1f} concurrent WGs")
