@@ -4,9 +4,11 @@
 # clock.  One counter group per rocprofv3 run, each under its own SIGKILL time limit; the first
 # failure ends the script.  tools/pmc_traffic.py folds them into OUT/traffic.json (bench.py
 # reads it from profiles/ when the library sha256 and the config match).
-#   gpurun --timeout 900 -- bash tools/gpu_pmc.sh TAG [CONFIG] [N_MG]
+#   gpurun --timeout 900 -- bash tools/gpu_pmc.sh TAG [CONFIG] [N_MG] [ENTRY]
+# ENTRY: the bench.py by_config name the counters stand for (default CONFIG; e.g. C4 100000
+# C4_100k): bench.py matches records by entry, so each batch size has its own.
 set -e -o pipefail
-TAG=${1:-pmc}; CFG=${2:-C2}; NMG=${3:-}
+TAG=${1:-pmc}; CFG=${2:-C2}; NMG=${3:-}; ENTRY=${4:-$CFG}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -30,5 +32,5 @@ pass lane SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU
 pass grbm GRBM_GUI_ACTIVE GRBM_COUNT
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE
-python3 tools/pmc_traffic.py "$OUT" repic-copy_amd/repic_amd/librepic_gc.so "$OUT/traffic.json" "$CFG" $((STEPS + WARM))
+python3 tools/pmc_traffic.py "$OUT" repic-copy_amd/repic_amd/librepic_gc.so "$OUT/traffic.json" "$CFG" $((STEPS + WARM)) "$ENTRY"
 echo "== done"

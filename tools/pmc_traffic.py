@@ -84,12 +84,14 @@ def main(argv):
         d, lib, out = argv[0], argv[1], argv[2]
         config = argv[3] if len(argv) > 3 else "C2"
         steps = int(argv[4]) if len(argv) > 4 else None
+        entry = argv[5] if len(argv) > 5 else config
         fetch, write = os.path.join(d, "fetch.csv"), os.path.join(d, "write.csv")
         extra = [os.path.join(d, f"{n}.csv") for n in ("sqa", "sqb", "grbm", "lane", "occ", "lds")]
         extra = [p for p in extra if os.path.exists(p)]
     else:
         fetch, write, lib, out = argv[:4]
         config = argv[4] if len(argv) > 4 else "C2"
+        entry = config
         steps = None
         extra = []
     f = per_kernel(fetch, {"FETCH_SIZE"})
@@ -110,7 +112,8 @@ def main(argv):
             e["counters"] = cnt[k]
             e["derived"] = derive(cnt[k])
         kernels[k] = e
-    res = {"lib_sha256": sha, "config": config, "unit": "bytes per launch",
+    # entry: the bench.py by_config name (the batch size: C4_100k is C4 at 100k micrographs)
+    res = {"lib_sha256": sha, "config": config, "entry": entry, "unit": "bytes per launch",
            "note": "FETCH_SIZE*1024 (raw, uncalibrated width) + WRITE_SIZE*1024; counters are "
                    "per-launch means, derived ratios per tools/pmc_traffic.py",
            "kernels": kernels}
