@@ -566,6 +566,7 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   LevelArgs L;
   L.D = 0; L.n_items = N; L.in_root = nullptr; L.in_M = nullptr; L.in_P = nullptr;
   L.cnt = nullptr; L.off = nullptr; L.out_root = nullptr; L.out_M = nullptr; L.out_P = nullptr;
+  L.next_cnt = nullptr;
   int cur = 0;
   int64_t C1 = 0, C2 = 0;
   for (int lv = 0; lv <= k - 2; ++lv) {
@@ -576,9 +577,12 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
     TRY(ensure_dev(c, D_TILES, scan_tiles_needed(L.n_items + 1) * 8));
     L.cnt = D<int32_t>(c, D_LCNT);
     L.off = D<int64_t>(c, D_LOFF);
-    TRY(mark(c, leaf ? "k5_leaf_count" : "k5_level_count"));
-    // (first level: L.cnt was zeroed with the per-box arrays; non-roots stay 0)
-    if (launch_clique_level(s, first, leaf, false, A, L) != 0) return fail("unsupported k");
+    // (the leaf level of k >= 3: its counts and marks came from the last fill, next_cnt)
+    if (!(leaf && k >= 3)) {
+      TRY(mark(c, leaf ? "k5_leaf_count" : "k5_level_count"));
+      // (first level: L.cnt was zeroed with the per-box arrays; non-roots stay 0)
+      if (launch_clique_level(s, first, leaf, false, A, L) != 0) return fail("unsupported k");
+    }
     launch_scan(s, L.n_items, L.cnt, D<int64_t>(c, D_LOFF), D<int64_t>(c, D_TILES), d_tot + 2);
     HIPCHK(hipMemcpyAsync(h_tot + 1, d_tot + 1, 16, hipMemcpyDeviceToHost, s));
     HIPCHK(hipGetLastError());
@@ -597,8 +601,17 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
     L.out_root = D<int32_t>(c, D_LROOT0 + o);
     L.out_M = D<uint64_t>(c, D_LM0 + o);
     L.out_P = D<uint64_t>(c, D_LP0 + o);
+    // the last fill's children are the leaf prefixes: it writes their leaf counts into the
+    // count buffer (this level's counts are dead after the scan; sized here so the leaf
+    // iteration's ensure_dev keeps it) and marks the clique vertices
+    L.next_cnt = nullptr;
+    if (lv == k - 3) {
+      TRY(ensure_dev(c, D_LCNT, nn * 4));
+      L.next_cnt = D<int32_t>(c, D_LCNT);
+    }
     TRY(mark(c, "k5_level_fill"));
     launch_clique_level(s, first, false, true, A, L);
+    L.next_cnt = nullptr;
     L.in_root = L.out_root; L.in_M = L.out_M; L.in_P = L.out_P;
     L.n_items = nn;
     cur = o;

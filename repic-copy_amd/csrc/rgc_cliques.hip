@@ -184,6 +184,65 @@ __global__ __launch_bounds__(WG) void k5l(CliqueArgs A, LevelArgs L) {
     }
     return;
   }
+  if constexpr (FILL && !LEAF) {
+    if (L.next_cnt) {   // (launch-uniform) the last fill: its children are the leaf prefixes
+      // Each child's cliques are the lanes m2 & pa (never empty: a child is kept only when it
+      // has one), so its leaf count goes to next_cnt and every member and leaf is a clique
+      // vertex: the leaf count pass is not needed.  The marks are OR-ed per root over the
+      // wave (its prefixes come grouped by root) and the run's last lane stores them, as the
+      // leaf count pass did.
+      const int lane = threadIdx.x & 63;
+      int r = -1 - lane;   // (lanes without a prefix: roots of their own, never joined)
+      uint64_t bits = 0;
+      int64_t lo = 0;
+      if (i < L.n_items && (!FIRST || A.rflag[(int)i])) {
+        r = FIRST ? (int)i : L.in_root[i];
+        const uint64_t M = FIRST ? ~0ull : L.in_M[i];
+        const uint64_t P = FIRST ? 0ull : L.in_P[i];
+        const int D = L.D;
+        const uint64_t rb = A.rbound[r];
+        lo = A.fwd_off[r];
+        uint64_t c = M & picker_lanes(rb, D + 1);
+        const uint64_t pa = picker_lanes(rb, D + 2);
+        int64_t o = L.off[i];
+        while (c) {
+          const int v = __builtin_ctzll(c);
+          c &= c - 1;
+          const uint64_t m2 = M & A.adjg[lo + v];
+          const uint64_t lv = m2 & pa;
+          if (lv) {
+            L.out_root[o] = r;
+            L.out_M[o] = lv;   // (a leaf prefix's mask matters only in its leaf picker)
+            L.out_P[o] = P | ((uint64_t)v << (6 * D));
+            L.next_cnt[o] = __popcll(lv);
+            bits |= lv | (1ull << v);
+            ++o;
+          }
+        }
+        if (bits)
+#pragma unroll
+          for (int q = 0; q < K - 3; ++q)
+            if (q < D) bits |= 1ull << ((P >> (6 * q)) & 63);
+      }
+#pragma unroll
+      for (int sft = 1; sft < 64; sft <<= 1) {
+        const uint64_t ob = __shfl_up(bits, sft, 64);
+        const int orr = __shfl_up(r, sft, 64);
+        if (lane >= sft && orr == r) bits |= ob;
+      }
+      const int nr = __shfl_down(r, 1, 64);
+      const bool tail = lane == 63 || nr != r;
+      if (r >= 0 && tail && bits) {
+        A.in_clique[r] = 1;
+        while (bits) {
+          const int v = __builtin_ctzll(bits);
+          bits &= bits - 1;
+          A.in_clique[A.e_dst[lo + v]] = 1;
+        }
+      }
+      return;
+    }
+  }
   if (i >= L.n_items) return;
   int r;
   uint64_t M, P;
@@ -747,7 +806,7 @@ __global__ __launch_bounds__(WG) RGC_EPI_WPE void k5_leaf_epi(CliqueArgs A, Leve
         const int r = L.in_root[i];
         const uint64_t P = L.in_P[i];
         lo = A.fwd_off[r];
-        c = L.in_M[i] & picker_lanes(A.rbound[r], L.D + 1);
+        c = L.in_M[i];   // (the last fill stored the leaf mask itself)
         s_m[wv][0][t] = r;
 #pragma unroll
         for (int u = 0; u < K - 2; ++u) s_m[wv][u + 1][t] = A.e_dst[lo + ((P >> (6 * u)) & 63)];

@@ -252,6 +252,8 @@ struct LevelArgs {
   int32_t* out_root;
   uint64_t* out_M;
   uint64_t* out_P;
+  int32_t* next_cnt;         // fill whose children are the leaf prefixes: their leaf counts
+                             // (and the clique-vertex marks), so no leaf count pass runs
 };
 
 void launch_clique_setup(hipStream_t stream, int N, const CliqueArgs& A);
