@@ -515,14 +515,14 @@ __global__ __launch_bounds__(WG) void k5_pack(int N, CliqueArgs A) {
 
 // Member gathers of one clique: COO rows (vertex ranks by (x, y, id), ascending) stored,
 // conf = f32(median score), the packed coordinates for the overlap paths.
-template <int K>
-__device__ __forceinline__ void epi_gather_mem(const CliqueArgs& A, int64_t j, const int (&mem)[K],
+template <int K, typename MemF>
+__device__ __forceinline__ void epi_gather_mem(const CliqueArgs& A, int64_t j, MemF&& mem,
                                                uint32_t (&xy)[K], float* conf32) {
   double s[K];
   int r[K];
 #pragma unroll
   for (int i = 0; i < K; ++i) {
-    const double2 p = reinterpret_cast<const double2*>(A.pk)[mem[i]];
+    const double2 p = reinterpret_cast<const double2*>(A.pk)[mem(i)];
     const uint64_t ry = (uint64_t)__double_as_longlong(p.y);
     s[i] = p.x;
     r[i] = (int)(uint32_t)ry;
@@ -538,13 +538,13 @@ __device__ __forceinline__ void epi_gather(const CliqueArgs& A, int64_t j, int (
                                            uint32_t (&xy)[K], float* conf32) {
 #pragma unroll
   for (int i = 0; i < K; ++i) mem[i] = A.members[j * K + i];
-  epi_gather_mem<K>(A, j, mem, xy, conf32);
+  epi_gather_mem<K>(A, j, [&](int i) { return mem[i]; }, xy, conf32);
 }
 
 // One clique's weighted-degree candidate and median JI: exact floats for integer coordinates
 // (k5_pack) and integer B <= 2896 (as the fused epilogue's INTP path), f64 otherwise.
-template <int K>
-__device__ __forceinline__ void epi_single(const CliqueArgs& A, const int (&mem)[K],
+template <int K, typename MemF>
+__device__ __forceinline__ void epi_single(const CliqueArgs& A, MemF&& mem,
                                            const uint32_t (&xy)[K], bool multi, bool* exact,
                                            int* arg, double* med) {
   const double B = A.B, two_b2 = A.two_b2;
@@ -562,7 +562,7 @@ __device__ __forceinline__ void epi_single(const CliqueArgs& A, const int (&mem)
   } else {
     double xs[K], ys[K];
 #pragma unroll
-    for (int i = 0; i < K; ++i) { xs[i] = A.x[mem[i]]; ys[i] = A.y[mem[i]]; }
+    for (int i = 0; i < K; ++i) { xs[i] = A.x[mem(i)]; ys[i] = A.y[mem(i)]; }
     epi_core<K, double>(xs, ys, B, two_b2, multi, exact, arg, med);
   }
 }
@@ -669,10 +669,13 @@ __device__ __forceinline__ uint64_t spread_even(uint64_t v) {
 // conf (epi_gather_mem), then w and the consensus; cliques that need the exact f64 pass get
 // their bit in exmask (zeroed before the launch; bit j & 63 of word j >> 6) and, with
 // ``keep_members``, their members for that pass.
-template <int K>
+// (mem(h, i): member i of clique h = 0 / 1, read where it is used: a caller that derives the
+// members from LDS does not hold 2 K of them in registers through the arithmetic)
+template <int K, typename MemF>
 __device__ __forceinline__ void epi_two(const CliqueArgs& A, int64_t j0, int64_t j1, bool two,
-                                        const int (&mem0)[K], const int (&mem1)[K],
-                                        bool keep_members) {
+                                        MemF&& mem, bool keep_members) {
+  auto mem0 = [&](int i) { return mem(0, i); };
+  auto mem1 = [&](int i) { return mem(1, i); };
   uint32_t xy0[K], xy1[K];
   float cf0, cf1 = 0.0f;
   epi_gather_mem<K>(A, j0, mem0, xy0, &cf0);
@@ -704,24 +707,18 @@ __device__ __forceinline__ void epi_two(const CliqueArgs& A, int64_t j0, int64_t
     atomicOr(reinterpret_cast<unsigned long long*>(A.exmask) + (j0 >> 6), 1ull << (j0 & 63));
     if (keep_members)
 #pragma unroll
-      for (int i = 0; i < K; ++i) A.members[j0 * K + i] = mem0[i];
+      for (int i = 0; i < K; ++i) A.members[j0 * K + i] = mem0(i);
   } else {
-    int cons = mem0[0];
-#pragma unroll
-    for (int i = 1; i < K; ++i) cons = (arg[0] == i) ? mem0[i] : cons;
-    A.consensus[j0] = cons;
+    A.consensus[j0] = mem0(arg[0]);
   }
   if (two) {
     if (ex[1]) {
       atomicOr(reinterpret_cast<unsigned long long*>(A.exmask) + (j1 >> 6), 1ull << (j1 & 63));
       if (keep_members)
 #pragma unroll
-        for (int i = 0; i < K; ++i) A.members[j1 * K + i] = mem1[i];
+        for (int i = 0; i < K; ++i) A.members[j1 * K + i] = mem1(i);
     } else {
-      int cons = mem1[0];
-#pragma unroll
-      for (int i = 1; i < K; ++i) cons = (arg[1] == i) ? mem1[i] : cons;
-      A.consensus[j1] = cons;
+      A.consensus[j1] = mem1(arg[1]);
     }
   }
 }
@@ -738,7 +735,12 @@ __global__ __launch_bounds__(WG) RGC_EPI_WPE void k5_epilogue(CliqueArgs A) {
   if (two)
 #pragma unroll
     for (int i = 0; i < K; ++i) mem1[i] = A.members[(j0 + 1) * K + i];
-  epi_two<K>(A, j0, j0 + 1, two, mem0, mem1, false);
+  epi_two<K>(A, j0, j0 + 1, two, [&](int h, int i) {
+    int v = mem0[0];
+#pragma unroll
+    for (int t = 0; t < K; ++t) v = i == t ? (h ? mem1[t] : mem0[t]) : v;
+    return v;
+  }, false);
 }
 
 // The level route's leaf level and the epilogue in one pass (k >= 3, outputs without
@@ -819,27 +821,29 @@ __global__ __launch_bounds__(WG) RGC_EPI_WPE void k5_leaf_epi(CliqueArgs A, Leve
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  auto members_of = [&](int q, int (&mem)[K]) {
+  // clique q: its prefix's staging slot and its leaf box
+  auto locate = [&](int q, int* slot, int* leaf) {
     // the last staged prefix whose first clique is <= q (s_off[0] <= 0)
     int a = 0;
 #pragma unroll
     for (int step = 64; step >= 1; step >>= 1)
       if (a + step < LE_Q && s_off[wv][a + step] <= q) a += step;
     const int v = select_bit(s_c[wv][a], q - s_off[wv][a]);   // the leaf's lane
-#pragma unroll
-    for (int t = 0; t < NM; ++t) mem[t] = s_m[wv][t][a];
-    mem[K - 1] = A.e_dst[s_lo[wv][a] + v];
+    *slot = a;
+    *leaf = A.e_dst[s_lo[wv][a] + v];
   };
   const int qa = lane, qb = lane + 64;
   if (j0 + qa >= C1) return;
   const bool two = j0 + qb < C1;
-  int mem0[K], mem1[K];
-  members_of(qa, mem0);
-  if (two) members_of(qb, mem1);
-  else
-#pragma unroll
-    for (int t = 0; t < K; ++t) mem1[t] = mem0[t];
-  epi_two<K>(A, j0 + qa, j0 + qb, two, mem0, mem1, true);
+  int sa, la, sb = 0, lb = 0;
+  locate(qa, &sa, &la);
+  if (two) locate(qb, &sb, &lb);
+  else { sb = sa; lb = la; }
+  // members read from the staging where they are used (the slots and leaf boxes stay live, not
+  // 2 K member ids: k = 8 spilled otherwise)
+  epi_two<K>(A, j0 + qa, j0 + qb, two, [&](int h, int i) {
+    return i == K - 1 ? (h ? lb : la) : s_m[wv][i][h ? sb : sa];
+  }, true);
 }
 
 // The deferred cliques as a list: one wave per 64 ballot words (4096 cliques) ranks their set
