@@ -42,7 +42,11 @@ BY_CONFIG = {"C2": ("C2", 10000), "C3": ("C3", 4000), "C4": ("C4", 12500), "C5":
              "C4_100k": ("C4", 100000), "C5_256": ("C5", 256),
              # strong scaling: ONE fixed 100k-micrograph C4 batch (the
              # north-star batch) split over the ranks, 100k / N each; at N = 1 it is C4_100k
-             "C4_100k_fixed": ("C4", 100000)}
+             "C4_100k_fixed": ("C4", 100000),
+             # C2 with fractional coordinates (3 decimals, as converted STAR / CBOX picks give):
+             # the fused kernel's f64 layout (untimed on the line before)
+             "C2_frac": ("C2", 10000)}
+ENTRY_KW = {"C2_frac": {"frac": True}}   # generator overrides of an entry
 FIXED_TOTAL = {"C4_100k_fixed"}   # entries whose micrograph count is the whole job's, not per GPU
 # file-to-file entries (the CLI on BOX text, one GPU, rank 0 of a 1-GPU run): C1 = the
 # reference's own EMPIAR-10017 example (12 micrographs, BASELINE configs[0]), C2_f2f = 10k
@@ -421,7 +425,8 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
     dist, world, rank, dev, cdev = env.dist, env.world, env.rank, env.dev, env.cdev
     depth = depth or PIPE_DEPTH.get(config, PIPE_DEPTH_DEFAULT)
     entry = entry or config
-    cfg = synth.SynthConfig(**synth.CONFIGS[config], seed=args.seed)
+    cfg = synth.SynthConfig(**dict(synth.CONFIGS[config], **ENTRY_KW.get(entry, {})),
+                            seed=args.seed)
     t_gen = time.time()
     # this rank's shard of one big batch (identical to packing synth.batch's list; large
     # batches are generated by a process pool)
@@ -576,7 +581,7 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
     out = {
         "value": value, "unit": "micrographs/s", "n_gpus": world, "steps": steps,
         "warmup": warmup, "ms_per_step": elapsed / steps * 1e3,
-        "config": {"workload": f"{config}: {synth.CONFIGS[config]}",
+        "config": {"workload": f"{entry}: {dict(synth.CONFIGS[config], **ENTRY_KW.get(entry, {}))}",
                    "micrographs_per_gpu": n_mg if fixed_total is None else fixed_total / world,
                    "micrographs_per_step": tot_mg,
                    "scaling": "weak" if fixed_total is None else "strong",
@@ -696,7 +701,7 @@ def main():
     # batch on this GPU), each with a 1-core CPU baseline sample on rank 0
     if args.by_config is None:
         extra = [] if args.n_mg else [c for c in ("C2", "C3", "C4", "C5", "C4_100k", "C5_256",
-                                                  "C4_100k_fixed", "C1", "C2_f2f")
+                                                  "C4_100k_fixed", "C2_frac", "C1", "C2_f2f")
                                       if c != args.config]
     elif args.by_config.lower() == "none":
         extra = []

@@ -74,7 +74,7 @@ enum DevBufId {
   D_IL_RPTR, D_IL_RCOLS, D_IL_CID, D_IL_CN, D_IL_COFF, D_IL_CCUR, D_IL_MEM, D_IL_LOC, D_IL_SCR,
   D_IL_BIG, D_IL_NBIG, D_IL_WSCR, D_IL_X, D_IL_EX, D_IL_RLOC, D_IL_CERT, D_IL_KEY, D_IL_ST,
   D_IL_RMAX, D_IL_OWN, D_IL_LAM, D_IL_GRAD, D_IL_CS, D_IL_CNT, D_IL_GAP, D_IL_STSAVE,
-  D_IL_FS, D_IL_FSCNT, D_IL_FSKEEP, D_LBUCKET,
+  D_IL_FS, D_IL_FSCNT, D_IL_FSKEEP, D_LBUCKET, D_WIDELIST,
   D_COUNT
 };
 enum HostBufId {
@@ -239,6 +239,7 @@ struct rgc_ctx {
   // shared by every context: streams beyond GPU_MAX_HW_QUEUES (4) share hardware queues
   bool copy_set = false;
   hipStream_t copy_stream = nullptr;
+  bool wide_hint = false;   // rgc_submit: the last batch had micrographs for the f64 layout
   hipEvent_t ev_k = nullptr;           // rgc_submit: after the fused launch
   uint64_t tiles_epoch = 0;      // scan_epoch_count() when D_TILES was last zeroed
   // rgc_submit's general path (host syncs per clique level) runs here; rgc_wait joins it
@@ -853,6 +854,8 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
       A.tie_list = D<int32_t>(c, D_TIES);
       A.tie_cap = c->cap_cliques;
       A.esum_n = 0;   // (the host sums the finished micrographs' edges from the stats copy)
+      A.wide_list = nullptr;   // (host-driven passes here)
+      A.mg_count = nullptr;
       int64_t ties_done = 0;   // entries of earlier passes already resolved
 #ifdef RGC_STAMPS
       TRY(ensure_dev(c, D_STAMPS, 3 * (size_t)n_mg * rgc::STAMP_SLOTS * 8));
@@ -1221,6 +1224,17 @@ static int submit_fast(rgc_ctx* c, const rgc_batch_in* in) {
   A.tie_list = D<int32_t>(c, D_TIES);
   A.tie_cap = c->cap_cliques;
   A.esum_n = n_mg;   // k_fused_ties sums the edges of the finished micrographs (cursor[1])
+  A.mg_count = nullptr;
+  // the last run on this context deferred micrographs to the f64 layout: this one appends its
+  // DEFER_WIDE micrographs to a device list and runs their f64 pass right after, on the
+  // stream (no host round trip, no rerun of the batch through the general path)
+  const FusedPlan* pw = c->wide_hint ? &cached_plan(k, 1, fused_class(nmaxb)) : nullptr;
+  if (pw && !pw->nmax) pw = nullptr;
+  A.wide_list = nullptr;
+  if (pw) {
+    TRY(ensure_dev(c, D_WIDELIST, (size_t)n_mg * 4));
+    A.wide_list = D<int32_t>(c, D_WIDELIST);
+  }
 #ifdef RGC_STAMPS
   return 0;   // the diagnostic build times through rgc_run only
 #endif
@@ -1249,6 +1263,19 @@ static int submit_fast(rgc_ctx* c, const rgc_batch_in* in) {
     TRY(mark(c, "k_fused"));
     const int le = launch_fused(s, nb, pl.lds, A, false, pl.nt);
     if (le != 0) return fail("fused kernel launch failed (submit): " +
+                             std::string(le > 0 ? hipGetErrorString((hipError_t)le) : "unsupported k"));
+  }
+  if (pw) {
+    FusedArgs Aw = A;
+    Aw.mg_list = A.wide_list;
+    Aw.mg_count = io.cur + 5;
+    Aw.wide_list = nullptr;
+    Aw.nmax = pw->nmax;
+    Aw.ecap = pw->ecap;
+    TRY(ensure_qg(c, Aw, k, pw->nt));
+    TRY(mark(c, "k_fused"));
+    const int le = launch_fused(s, n_mg, pw->lds, Aw, true, pw->nt);
+    if (le != 0) return fail("fused f64 kernel launch failed (submit): " +
                              std::string(le > 0 ? hipGetErrorString((hipError_t)le) : "unsupported k"));
   }
   TRY(mark(c, "k_fused_ties"));
@@ -1299,6 +1326,9 @@ static int wait_fast(rgc_ctx* c, rgc_batch_out* out) {
   const unsigned long long* h_cur = reinterpret_cast<const unsigned long long*>(
       H<char>(c, H_MGOUT) + cur_off + c->pend_slot * CUR_BYTES);
   bool again = (int64_t)h_cur[0] > c->cap_cliques || h_cur[4] != 0;
+  // the next submit on this context runs the f64 pass on the device when this batch had
+  // micrographs for it
+  c->wide_hint = h_cur[5] != 0;
   const bool lazy = (in->flags & RGC_F_LAZY_STATS) != 0;
   for (int m = 0; m < n_mg && !again && !lazy; ++m) again = ho.status[m] >= RGC_ST_DEFER;
   if (again) return 0;

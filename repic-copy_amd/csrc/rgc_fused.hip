@@ -1059,7 +1059,16 @@ __device__ __forceinline__ void put_stats(const FusedArgs& A, int m, int status,
   A.o.clique_base[m] = base;
   A.o.clique_cnt[m] = C;
   // a micrograph that needs another pass is counted, so a run's totals alone tell the host
-  // (lazy stats); the edges of finished ones are summed after the launch (k_fused_ties)
+  // (lazy stats); the edges of finished ones are summed after the launch (k_fused_ties).
+  // DEFER_WIDE ones are also counted on cursor[5]; with a device-side f64 pass to follow
+  // (wide_list) they go to its list and are not a deferral for the host
+  if (status == RGC_ST_DEFER_WIDE) {
+    const unsigned long long q = atomicAdd(A.cursor + 5, 1ull);
+    if (A.wide_list) {
+      A.wide_list[q] = m;
+      return;
+    }
+  }
   if (!(status == 0 || status == RGC_ST_NO_CLIQUES || status == RGC_ST_NO_EDGES))
     atomicAdd(A.cursor + 4, 1ull);
 }
@@ -1118,6 +1127,8 @@ void k_fused(FusedArgs A) {
   S.dst = reinterpret_cast<uint16_t*>(smem + L.off_dst);
   S.cbuf = reinterpret_cast<uint16_t*>(smem + L.off_cbuf);
   const int tid = threadIdx.x;
+  // (device-side f64 pass: the list's length is known on the device only)
+  if (A.mg_count && blockIdx.x >= *A.mg_count) return;
   const int m = A.mg_list ? A.mg_list[blockIdx.x] : (int)blockIdx.x;
   if (blockIdx.x == 0 && tid < 16 && A.cursor_clear) A.cursor_clear[tid] = 0;   // next run's
 #ifdef RGC_STAMPS

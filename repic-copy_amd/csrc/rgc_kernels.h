@@ -106,7 +106,8 @@ struct FusedArgs {
   MgOut o;                      // per-micrograph outputs (device)
   // [0] clique-range reservation, [1] edges of finished mgs (summed by k_fused_ties over the
   // first esum_n micrographs' stats; no per-workgroup atomic: 10k workgroups adding to one
-  // word cost ~8 % of C2's kernel), [2] edge dump, [4] deferrals, [CUR_TIES] ties
+  // word cost ~8 % of C2's kernel), [2] edge dump, [4] deferrals, [5] f32-pass micrographs
+  // deferred to the f64 layout (DEFER_WIDE), [CUR_TIES] ties
   unsigned long long* cursor;
   // cursors of the context's other run slot: zeroed by block 0 for the next run (no memset
   // packet between runs)
@@ -136,6 +137,12 @@ struct FusedArgs {
   int32_t* tie_list;
   int64_t tie_cap;
   int esum_n;   // k_fused_ties: micrographs whose finished edges it sums into cursor[1]
+  // device-side f64 pass (rgc_submit): the f32 pass appends its DEFER_WIDE micrographs to
+  // wide_list (count cursor[5]) instead of counting them as deferrals; the f64 launch that
+  // follows on the stream takes mg_list = wide_list with mg_count = cursor + 5 (blocks past
+  // the count exit at once), so no host round trip sits between the two passes
+  int32_t* wide_list;
+  const unsigned long long* mg_count;
 };
 
 int fused_lds_bytes(int nmax, int ecap, bool wide);
