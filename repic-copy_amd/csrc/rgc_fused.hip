@@ -683,10 +683,10 @@ struct BfsLevel {
     return S.split[m];
   }
 
-  template <bool REWALK>
+  template <bool REWALK, typename EP>
   __device__ __forceinline__ static BfsOut<K> run(const FShared& S, FusedHdr& H, char* q,
                                                   int qbytes, BfsOut<K>& out, int64_t nD, int tid,
-                                                  const int (&pp)[K + 1]) {
+                                                  const int (&pp)[K + 1], const EP& ep) {
     int (&lvl)[K + 1] = out.lvl;
     constexpr int ES = bfs_es<WE>();
     // temps of this level at the top of q
@@ -708,17 +708,20 @@ struct BfsLevel {
       const int m = mm[D - 1];
       const int lo = S.fwd[m], hi = seg_end<REWALK>(S, pp, m);
       uint32_t mask = 0, cnt = 0;
-      // an extension h (picker D) lies past member mm[d]'s first segment (picker d + 1 < D):
-      // search from split (dead in REWALK: the whole list)
-      int slo[K > 2 ? K - 2 : 1];
+      // an extension h (picker D) must be adjacent to every earlier member: the graph's edges
+      // are exactly the pairs of different pickers with JI > 0.3, so instead of a binary
+      // search of h in each member's sorted list (three dependent LDS loads each), P2's own
+      // test on the two boxes' coordinates decides it (ep.edge: the same function on the same
+      // LDS values, so the same answer); the members' coordinates stay in registers
+      typename EP::CT mc[K > 2 ? K - 2 : 1];
 #pragma unroll
-      for (int d = 0; d < D - 1; ++d) slo[d] = REWALK ? (int)S.fwd[mm[d]] : (int)S.split[mm[d]];
+      for (int d = 0; d < D - 1; ++d) mc[d] = ep.pt(S, mm[d]);
       for (int t = lo; t < hi; ++t) {
         const int h = S.dst[t];
+        const typename EP::CT ch = ep.pt(S, h);
         bool ok = true;
 #pragma unroll
-        for (int d = 0; d < D - 1; ++d)
-          ok = ok && contains16(S.dst, slo[d], S.fwd[mm[d] + 1], h);
+        for (int d = 0; d < D - 1; ++d) ok &= ep.edge(mc[d], ch);
         cnt += ok ? 1u : 0u;
         mask |= (ok && t - lo < 32) ? (1u << (t - lo)) : 0u;
       }
@@ -752,10 +755,10 @@ struct BfsLevel {
         if (t - lo < 32) {
           ok = (mask >> (t - lo)) & 1u;
         } else {
+          const typename EP::CT ch = ep.pt(S, h);
           ok = true;
 #pragma unroll
-          for (int d = 0; d < D - 1; ++d)
-            ok = ok && contains16(S.dst, S.fwd[mm[d]], S.fwd[mm[d] + 1], h);
+          for (int d = 0; d < D - 1; ++d) ok &= ep.edge(ep.pt(S, mm[d]), ch);
         }
         if (!ok) continue;
         if constexpr (WE) {
@@ -780,7 +783,7 @@ struct BfsLevel {
     __syncthreads();
     lvl[D + 1] = nb;
     if constexpr (D + 1 < K) {
-      return BfsLevel<K, D + 1, NT, WE>::template run<REWALK>(S, H, q, qbytes, out, nN, tid, pp);
+      return BfsLevel<K, D + 1, NT, WE>::template run<REWALK>(S, H, q, qbytes, out, nN, tid, pp, ep);
     } else {
       out.C = nN;
       return out;
@@ -791,11 +794,11 @@ struct BfsLevel {
 // Cliques of the roots [r0, r1) (picker-0 positions).  Returns C = -1 when a level does not
 // fit the queue region; the caller then retries with fewer roots (root chunks, P4) and falls
 // back to the per-root DFS only when a single root does not fit.
-template <int K, bool REWALK, int NT, bool WE = false>
+template <int K, bool REWALK, int NT, bool WE = false, typename EP>
 __device__ __forceinline__ BfsOut<K> bfs_cliques(const FShared& S, FusedHdr& H, char* q,
                                                  int qbytes, int r0, int r1, bool get_cc,
                                                  uint32_t target, int tid,
-                                                 const int (&pp)[K + 1]) {
+                                                 const int (&pp)[K + 1], const EP& ep) {
   BfsOut<K> out;
   out.C = -1;
   out.fit = 4.0f;
@@ -846,7 +849,7 @@ __device__ __forceinline__ BfsOut<K> bfs_cliques(const FShared& S, FusedHdr& H, 
   __syncthreads();
   out.lvl[2] = 0;
   if constexpr (K > 2) {
-    return BfsLevel<K, 2, NT, WE>::template run<REWALK>(S, H, q, qbytes, out, n2, tid, pp);
+    return BfsLevel<K, 2, NT, WE>::template run<REWALK>(S, H, q, qbytes, out, n2, tid, pp, ep);
   } else {
     out.C = n2;
     return out;
@@ -933,6 +936,27 @@ __device__ __forceinline__ bool edge_test(double2 a, double2 b, double B, double
   if (!e && inter >= i_lo) e = inter / (two_b2 - inter) > 0.3;   // reference quotient
   return e;
 }
+
+// P2's edge decision on two boxes' LDS coordinates (lower picker first), for P4's adjacency
+// tests: the integer test of pairs_count_int on the f32 layout, edge_test on the f64 layout
+template <bool W>
+struct EdgeP {
+  using CT = typename std::conditional<W, double2, float2>::type;
+  float Bf, Tf;
+  double B, two_b2, ilo, ihi;
+  __device__ __forceinline__ CT pt(const FShared& S, int p) const {
+    return reinterpret_cast<const CT*>(S.sxy)[p];
+  }
+  __device__ __forceinline__ bool edge(CT a, CT b) const {
+    if constexpr (W) {
+      return edge_test(a, b, B, two_b2, ilo, ihi);
+    } else {
+      const float xo = fmaxf(Bf - fabsf(a.x - b.x), 0.0f);
+      const float yo = fmaxf(Bf - fabsf(a.y - b.y), 0.0f);
+      return xo * yo > Tf;
+    }
+  }
+};
 
 // P2 count for the box at sorted position ts (thread per box): JI test against every stencil
 // candidate of a higher picker; returns the edge count and, for the fill, either the targets
@@ -1384,6 +1408,7 @@ void k_fused(FusedArgs A) {
   // pass decides every candidate with six f32 operations (edge_test_int)
   // (the f32 layout is integer-only: P0)
   const int ti = W ? 0 : (6 * (int)B * (int)B) / 13;
+  const EdgeP<W> ep{(float)B, (float)ti, B, two_b2, i_lo, i_hi};   // (P4's adjacency tests)
   // thread per box (sorted position): lanes of a wave hold neighbouring boxes of one picker,
   // so their stencils overlap (similar trip counts, broadcast LDS reads), and the waves of
   // picker K-1 have nothing to do.  cnt[] (dead until P3) keeps
@@ -1663,10 +1688,10 @@ void k_fused(FusedArgs A) {
       len = min(len, n0 - r0);
       if (QG && K <= 4 && qslot >= 0)
         bo = bfs_cliques<K, false, NT, QG && K <= 4>(S, H, q, qbytes, r0, r0 + len, get_cc,
-                                                     (uint32_t)target, tid, c.pp);
+                                                     (uint32_t)target, tid, c.pp, ep);
       else
         bo = bfs_cliques<K, false, NT>(S, H, q, qbytes, r0, r0 + len, get_cc, (uint32_t)target,
-                                       tid, c.pp);
+                                       tid, c.pp, ep);
       if (bo.C < 0) {
         // shrink to the estimated fit of the overflowing level (demand grows about linearly
         // with the roots), with a small margin; strictly smaller each time
@@ -1838,10 +1863,10 @@ void k_fused(FusedArgs A) {
           if (ci > 0)
             cur = we ? bfs_cliques<K, true, NT, QG && K <= 4>(S, H, q, qbytes, ufl((int)chtab[2 * ch]),
                                        ufl((int)chtab[2 * ch + 2]), get_cc, (uint32_t)target,
-                                       tid, c.pp)
+                                       tid, c.pp, ep)
                      : bfs_cliques<K, true, NT>(S, H, q, qbytes, ufl((int)chtab[2 * ch]),
                                        ufl((int)chtab[2 * ch + 2]), get_cc, (uint32_t)target,
-                                       tid, c.pp);
+                                       tid, c.pp, ep);
         }
         c.cq_ord = reinterpret_cast<uint16_t*>(q + cur.lvl[K] + (we ? 8 : 4) * (c1 - c0));
       } else {
