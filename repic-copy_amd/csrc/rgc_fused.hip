@@ -656,13 +656,15 @@ __device__ __forceinline__ uint2 we_pack(const int (&mm)[4], int d, int h) {
 template <int K, int D, int NT, bool WE = false>
 struct BfsLevel {
   // prefix members of entry e of level D (D members, compile-time indices only)
+  __device__ __forceinline__ static void unpack(const uint2 v, int (&mm)[K]) {
+    const int t[4] = {(int)(v.x & 0xFFFF), (int)(v.x >> 16), (int)(v.y & 0xFFFF), (int)(v.y >> 16)};
+#pragma unroll
+    for (int d = 0; d < D && d < 4; ++d) mm[d] = t[d];
+  }
   __device__ __forceinline__ static void prefix(const char* q, const int (&lvl)[K + 1],
                                                 uint32_t e, int (&mm)[K]) {
     if constexpr (WE) {
-      const uint2 v = reinterpret_cast<const uint2*>(q + lvl[D])[e];
-      const int t[4] = {(int)(v.x & 0xFFFF), (int)(v.x >> 16), (int)(v.y & 0xFFFF), (int)(v.y >> 16)};
-#pragma unroll
-      for (int d = 0; d < D; ++d) mm[d] = t[d];
+      unpack(reinterpret_cast<const uint2*>(q + lvl[D])[e], mm);
       return;
     }
     uint32_t ent = reinterpret_cast<const uint32_t*>(q + lvl[D])[e];
@@ -1904,15 +1906,45 @@ void k_fused(FusedArgs A) {
         return (c.cq_ord[sl] & 0x8000) != 0;
       };
       bool any = false;
-      for (int sl = tid; sl < c1 - c0; sl += FWG) {
-        int mem[K];
-        const int64_t jo = clique_members(sl, mem);
+      auto epi = [&](int sl, int (&mem)[K]) {
+        const int64_t jo = obase + (c0 + sl);
         bool order;
         if constexpr (!W) order = fused_epilogue_main<K, W, true>(c, jo, mem);
         else order = fused_epilogue_main<K, W, false>(c, jo, mem);
         if (order) {
           set_order_flag(sl);
           any = true;
+        }
+      };
+      if constexpr (QG && K <= 4) {
+        if (bfs_ok && we) {
+          // wide entries in the HBM slot: the next clique's members are loaded before this
+          // one's epilogue runs (an L2 round trip per clique otherwise sits on the chain)
+          const uint2* ent = reinterpret_cast<const uint2*>(q + cur.lvl[K]);
+          const int cnt = c1 - c0;
+          uint2 nx = tid < cnt ? ent[tid] : make_uint2(0u, 0u);
+          for (int sl = tid; sl < cnt; sl += FWG) {
+            const uint2 v = nx;
+            if (sl + FWG < cnt) nx = ent[sl + FWG];
+            const int t[4] = {(int)(v.x & 0xFFFF), (int)(v.x >> 16), (int)(v.y & 0xFFFF),
+                              (int)(v.y >> 16)};
+            int mem[K];
+#pragma unroll
+            for (int i = 0; i < K; ++i) mem[i] = t[i];
+            epi(sl, mem);
+          }
+        } else {
+          for (int sl = tid; sl < c1 - c0; sl += FWG) {
+            int mem[K];
+            clique_members(sl, mem);
+            epi(sl, mem);
+          }
+        }
+      } else {
+        for (int sl = tid; sl < c1 - c0; sl += FWG) {
+          int mem[K];
+          clique_members(sl, mem);
+          epi(sl, mem);
         }
       }
       if (any) H.tief[ci & 1] = 1;
