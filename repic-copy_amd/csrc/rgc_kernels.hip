@@ -71,6 +71,8 @@ __global__ __launch_bounds__(1024) void k1_bin(int k, double B, const int32_t* _
   if (threadIdx.x == 0) notint = !(B >= 1.0 && B <= 2896.0 && B == floor(B));
   double mnx = INFINITY, mny = INFINITY, mxx = -INFINITY, mxy = -INFINITY;
   bool ni = false;
+  // (one workgroup per micrograph: the loops over its boxes keep four loads in flight)
+#pragma unroll 4
   for (int i = threadIdx.x; i < n; i += BT) {
     const double xv = x[b0 + i], yv = y[b0 + i];
     if (isfinite(xv) && isfinite(yv)) {
@@ -127,6 +129,7 @@ __global__ __launch_bounds__(1024) void k1_bin(int k, double B, const int32_t* _
     for (int q = 1; q < k; ++q) p += i >= poff[q] ? 1 : 0;
     return p;
   };
+#pragma unroll 4
   for (int i = threadIdx.x; i < n; i += BT) {
     const int q = bin_key(G, picker(i), x[b0 + i], y[b0 + i]);
     if (WIDE) atomicAdd(&cntw[q], 1u);
@@ -158,6 +161,7 @@ __global__ __launch_bounds__(1024) void k1_bin(int k, double B, const int32_t* _
     }
   }
   __syncthreads();
+#pragma unroll 4
   for (int i = threadIdx.x; i < n; i += BT) {
     const int g = b0 + i;
     const double xv = x[g], yv = y[g];
@@ -208,14 +212,13 @@ __global__ __launch_bounds__(WG) void k2_pairs(int N, int k, double B, double tw
   int cnt = 0;
   int64_t base = 0;
   if (FILL) base = fwd_off[g];
-  // fill: up to FILL_REGS targets stay in registers and are sorted by a compare-exchange
-  // network (an insertion sort through global memory costs a dependent L2 round trip per
-  // shift); longer lists, and the RGC_F_EDGES dump with its JIs, go through e_dst
+  // fill: each higher picker's targets (a segment of the sorted list: box indices are
+  // picker-major) collect in registers, up to FILL_REGS of them, and are sorted there by a
+  // compare-exchange network (an insertion sort through global memory costs a dependent L2
+  // round trip per shift; C5's picker-0 boxes have ~7-20 targets over 7 pickers, one to three
+  // per picker); a longer segment, and the RGC_F_EDGES dump with its JIs, go through e_dst
   constexpr int FILL_REGS = 8;
   const bool reg = FILL && e_ji == nullptr;
-  int rk[FILL_REGS];
-#pragma unroll
-  for (int i = 0; i < FILL_REGS; ++i) rk[i] = INT32_MAX;
   const int key = bin_key(G, p, xa, ya);
   if (key < G.nkey && p + 1 < k) {
     const int cell = key - p * G.ncell;
@@ -231,6 +234,11 @@ __global__ __launch_bounds__(WG) void k2_pairs(int N, int k, double B, double tw
     const double t_star = 0.6 * B * B / 1.3;
     const double i_lo = t_star * (1.0 - 0x1p-40), i_hi = t_star * (1.0 + 0x1p-40);
     for (int q = p + 1; q < k; ++q) {
+      int rk[FILL_REGS];
+#pragma unroll
+      for (int i = 0; i < FILL_REGS; ++i) rk[i] = INT32_MAX;
+      const int64_t sb = base + cnt;   // (fill) this picker's segment
+      int cq = 0;
       for (int d = 0; d <= 1; ++d) {
         const int col = sc + d;
         if (col < 0 || col >= G.gx) continue;
@@ -252,17 +260,17 @@ __global__ __launch_bounds__(WG) void k2_pairs(int N, int k, double B, double tw
           }
           if (e) {
             if (FILL) {
-              if (reg) {   // the first FILL_REGS targets in a register shift chain
-                if (cnt == FILL_REGS) {   // more: spill them in arrival order, then write through
+              if (reg) {   // a register shift chain; more: spill in arrival order, write through
+                if (cq == FILL_REGS) {
 #pragma unroll
-                  for (int i = 0; i < FILL_REGS; ++i) e_dst[base + i] = rk[FILL_REGS - 1 - i];
+                  for (int i = 0; i < FILL_REGS; ++i) e_dst[sb + i] = rk[FILL_REGS - 1 - i];
                 }
-                if (cnt < FILL_REGS) {
+                if (cq < FILL_REGS) {
 #pragma unroll
                   for (int i = FILL_REGS - 1; i > 0; --i) rk[i] = rk[i - 1];
                   rk[0] = sbox[v];
                 } else {
-                  e_dst[base + cnt] = sbox[v];
+                  e_dst[sb + cq] = sbox[v];
                 }
               } else {
                 e_dst[base + cnt] = sbox[v];
@@ -270,6 +278,25 @@ __global__ __launch_bounds__(WG) void k2_pairs(int N, int k, double B, double tw
               }
             }
             ++cnt;
+            ++cq;
+          }
+        }
+      }
+      if (reg && cq > 0) {
+        if (cq <= FILL_REGS) {
+          cmpnet_apply<FILL_REGS, false>(rk);   // ascending; unused slots hold INT32_MAX
+#pragma unroll
+          for (int i = 0; i < FILL_REGS; ++i)
+            if (i < cq) e_dst[sb + i] = rk[i];
+        } else {
+          for (int i = 1; i < cq; ++i) {   // (rare) insertion sort of the segment
+            const int kd = e_dst[sb + i];
+            int j = i - 1;
+            while (j >= 0 && e_dst[sb + j] > kd) {
+              e_dst[sb + j + 1] = e_dst[sb + j];
+              --j;
+            }
+            e_dst[sb + j + 1] = kd;
           }
         }
       }
@@ -277,24 +304,19 @@ __global__ __launch_bounds__(WG) void k2_pairs(int N, int k, double B, double tw
   }
   if (!FILL) {
     fwd_cnt[g] = cnt;
-  } else if (reg && cnt <= FILL_REGS) {
-    cmpnet_apply<FILL_REGS, false>(rk);   // ascending; unused slots hold INT32_MAX
-#pragma unroll
-    for (int i = 0; i < FILL_REGS; ++i)
-      if (i < cnt) e_dst[base + i] = rk[i];
-  } else {
+  } else if (!reg) {
     // insertion sort by target box (each picker's segment arrives in cell order)
     for (int i = 1; i < cnt; ++i) {
       const int kd = e_dst[base + i];
-      const double kj = e_ji ? e_ji[base + i] : 0.0;
+      const double kj = e_ji[base + i];
       int j = i - 1;
       while (j >= 0 && e_dst[base + j] > kd) {
         e_dst[base + j + 1] = e_dst[base + j];
-        if (e_ji) e_ji[base + j + 1] = e_ji[base + j];
+        e_ji[base + j + 1] = e_ji[base + j];
         --j;
       }
       e_dst[base + j + 1] = kd;
-      if (e_ji) e_ji[base + j + 1] = kj;
+      e_ji[base + j + 1] = kj;
     }
   }
 }
@@ -508,23 +530,37 @@ __global__ __launch_bounds__(1024) void k4_union_lds(int k, const int32_t* __res
   const int b0 = box_off[m * k], n = box_off[m * k + k] - b0;
   for (int i = threadIdx.x; i < n; i += 1024) P[i] = i;
   __syncthreads();
+  // one workgroup per micrograph (C5: 64 of 256 CUs, ~27 boxes and ~270 unions per thread):
+  // the global loads are the latency chain, so a box's targets are read UF_B at a time and
+  // the next box's edge range is loaded before this box's unions
+  constexpr int UF_B = 8;
+  int64_t e0 = 0, e1 = 0;
+  if (threadIdx.x < n) { e0 = fwd_off[b0 + threadIdx.x]; e1 = fwd_off[b0 + threadIdx.x + 1]; }
   for (int i = threadIdx.x; i < n; i += 1024) {
-    const int64_t e0 = fwd_off[b0 + i], e1 = fwd_off[b0 + i + 1];
-    if (e0 == e1) continue;
+    const int64_t c0 = e0, c1 = e1;
+    if (i + 1024 < n) { e0 = fwd_off[b0 + i + 1024]; e1 = fwd_off[b0 + i + 1025]; }
+    if (c0 == c1) continue;
     has_edge[b0 + i] = 1;
-    for (int64_t e = e0; e < e1; ++e) {
-      const int h = e_dst[e] - b0;
-      has_edge[b0 + h] = 1;
-      int a = i, b = h;
-      for (;;) {
-        a = uf_find_l(P, a);
-        b = uf_find_l(P, b);
-        if (a == b) break;
-        if (a < b) { const int t = a; a = b; b = t; }
-        int expect = a;
-        if (__hip_atomic_compare_exchange_strong(P + a, &expect, b, __ATOMIC_RELAXED,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-          break;
+    for (int64_t e = c0; e < c1; e += UF_B) {
+      int hs[UF_B];
+#pragma unroll
+      for (int u = 0; u < UF_B; ++u) hs[u] = e + u < c1 ? e_dst[e + u] - b0 : -1;
+#pragma unroll
+      for (int u = 0; u < UF_B; ++u) {
+        const int h = hs[u];
+        if (h < 0) continue;
+        has_edge[b0 + h] = 1;
+        int a = i, b = h;
+        for (;;) {
+          a = uf_find_l(P, a);
+          b = uf_find_l(P, b);
+          if (a == b) break;
+          if (a < b) { const int t = a; a = b; b = t; }
+          int expect = a;
+          if (__hip_atomic_compare_exchange_strong(P + a, &expect, b, __ATOMIC_RELAXED,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+            break;
+        }
       }
     }
   }
@@ -538,7 +574,12 @@ __global__ __launch_bounds__(WG) void k4_compress(int N, const uint8_t* __restri
   if (g >= N || !has_edge[g]) return;
   const int r = uf_find(parent, g);
   __hip_atomic_store(parent + g, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  atomicAdd(&csize[r], 1);
+  // the lanes in the first active lane's component add once (a dense micrograph's giant
+  // component would otherwise queue one atomic per box on one address)
+  const int rf = __builtin_amdgcn_readfirstlane(r);
+  const uint64_t same = __ballot(r == rf);
+  if (r != rf) atomicAdd(&csize[r], 1);
+  else if (__lane_id() == __builtin_ctzll(same)) atomicAdd(&csize[r], (int)__popcll(same));
 }
 
 // Per-micrograph CC statistics (runtime.tsv columns 2-3) and NO_EDGES status.
@@ -553,11 +594,13 @@ __global__ __launch_bounds__(WG) void k4_stats(int k, const int32_t* __restrict_
   const int b0 = box_off[m * k], b1 = box_off[m * k + k];
   int64_t nodes = 0, roots = 0;
   int mx = 0;
+  // (one workgroup per micrograph: loads of four boxes in flight per thread)
+#pragma unroll 4
   for (int g = b0 + threadIdx.x; g < b1; g += WG) {
-    if (has_edge[g]) {
-      ++nodes;
-      if (parent[g] == g) { ++roots; mx = max(mx, csize[g]); }
-    }
+    const bool he = has_edge[g];
+    const bool root = parent[g] == g;
+    nodes += he ? 1 : 0;
+    if (he && root) { ++roots; mx = max(mx, csize[g]); }
   }
   nodes = block_sum64(nodes, red);
   roots = block_sum64(roots, red);
