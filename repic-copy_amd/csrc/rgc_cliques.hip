@@ -661,8 +661,11 @@ __device__ __forceinline__ uint64_t spread_even(uint64_t v) {
 // Same arithmetic as the fused kernel's epilogue (rgc_fused.hip fused_epilogue_main / _order).
 // Thread t takes cliques 2t and 2t + 1: the packed-u16 pair path when both qualify, one at a
 // time otherwise.
+// (4 waves per SIMD: the k = 8 instances spill 80 bytes per lane to fit 128 VGPRs and still
+// run 2.0 % (C5) / 2.4 % (C5_256) faster than at 3 without spills; 5 and 6 waves spill
+// 356 / 500 bytes and run 29 % / 46 % slower: profiles/r06al_*, r06am_*)
 #ifndef RGC_EPI_WPE_N
-#define RGC_EPI_WPE_N 3
+#define RGC_EPI_WPE_N 4
 #endif
 #define RGC_EPI_WPE __attribute__((amdgpu_waves_per_eu(RGC_EPI_WPE_N)))
 // The epilogue of cliques j0 and j1 (j1 only with ``two``) whose members are known: rows and
@@ -778,8 +781,7 @@ __global__ __launch_bounds__(WG) void k5_leaf_bucket(LevelArgs L, int32_t* bucke
   for (int64_t b = (lo + LE_Q - 1) / LE_Q; b * LE_Q < hi; ++b) bucket[b] = (int32_t)i;
 }
 
-// (k = 8 spills 64 bytes per lane at 3 waves per SIMD; at 2 waves per SIMD, no spill, it ran
-// 15 % slower: profiles/r06l_*)
+// (k = 8 at 2 waves per SIMD ran 15 % slower than at 3: profiles/r06l_*; 4: RGC_EPI_WPE_N)
 template <int K>
 __global__ __launch_bounds__(WG) RGC_EPI_WPE void k5_leaf_epi(CliqueArgs A, LevelArgs L,
                                                            const int32_t* bucket, int64_t C1) {
@@ -881,6 +883,8 @@ __global__ __launch_bounds__(WG) void k5_ex_write(CliqueArgs A) {
 // weighted degrees (get_cliques.py:182-183) and, on ties, the first tied member in networkx's
 // node-iteration order (CPython set order of (x, y, id), or graph insertion order when
 // 2k >= |G|).  Grid-stride over the deferred list.
+// (k = 8: 159 VGPRs, 3 waves per SIMD; forced to 4 it spills 92 bytes and runs 1 % slower
+// per C5 step: profiles/r06an_*)
 template <int K>
 __global__ __launch_bounds__(WG) void k5_epi_exact(CliqueArgs A) {
   const int64_t n = (int64_t)*A.excount;

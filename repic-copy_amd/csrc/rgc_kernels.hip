@@ -71,8 +71,6 @@ __global__ __launch_bounds__(1024) void k1_bin(int k, double B, const int32_t* _
   if (threadIdx.x == 0) notint = !(B >= 1.0 && B <= 2896.0 && B == floor(B));
   double mnx = INFINITY, mny = INFINITY, mxx = -INFINITY, mxy = -INFINITY;
   bool ni = false;
-  // (one workgroup per micrograph: the loops over its boxes keep four loads in flight)
-#pragma unroll 4
   for (int i = threadIdx.x; i < n; i += BT) {
     const double xv = x[b0 + i], yv = y[b0 + i];
     if (isfinite(xv) && isfinite(yv)) {
@@ -129,7 +127,6 @@ __global__ __launch_bounds__(1024) void k1_bin(int k, double B, const int32_t* _
     for (int q = 1; q < k; ++q) p += i >= poff[q] ? 1 : 0;
     return p;
   };
-#pragma unroll 4
   for (int i = threadIdx.x; i < n; i += BT) {
     const int q = bin_key(G, picker(i), x[b0 + i], y[b0 + i]);
     if (WIDE) atomicAdd(&cntw[q], 1u);
@@ -161,7 +158,6 @@ __global__ __launch_bounds__(1024) void k1_bin(int k, double B, const int32_t* _
     }
   }
   __syncthreads();
-#pragma unroll 4
   for (int i = threadIdx.x; i < n; i += BT) {
     const int g = b0 + i;
     const double xv = x[g], yv = y[g];
