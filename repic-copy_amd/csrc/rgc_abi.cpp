@@ -618,11 +618,12 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
     cur = o;
   }
   // row ranks need only the clique-vertex flags of the count passes (bucket counters in
-  // D_VLIST, slots in D_CSIZE: the CC sizes are dead by now)
+  // D_VLIST, slots in D_CSIZE: the CC sizes are dead by now; buckets in D_FWDCNT, dead since
+  // the edge scan)
   TRY(mark(c, "k7_rank"));
   launch_rank(s, (int)N, n_mg, k, bo, D<int32_t>(c, D_BMG), D<MgGrid>(c, D_GRID), x, y,
               D<uint8_t>(c, D_INCL), D<int32_t>(c, D_VLIST), D<int32_t>(c, D_CSIZE),
-              D<int64_t>(c, D_BOFF), D<int64_t>(c, D_TILES), d_tot + 3,
+              D<int32_t>(c, D_FWDCNT), D<int64_t>(c, D_BOFF), D<int64_t>(c, D_TILES), d_tot + 3,
               D<int32_t>(c, D_VSORT), D<int32_t>(c, D_VROW), D<MgStat>(c, D_STAT));
   const int64_t C = C1 + C2;
   *C_out = C;

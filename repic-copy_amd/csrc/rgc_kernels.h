@@ -277,8 +277,9 @@ void launch_clique_ranges(hipStream_t stream, const CliqueArgs& A, int64_t C1, i
 int launch_cliques_dfs(hipStream_t stream, bool fill, int N, const CliqueArgs& A);
 void launch_rank(hipStream_t stream, int N, int n_mg, int k, const int32_t* box_off,
                  const int32_t* bmg, const MgGrid* grid, const double* x, const double* y,
-                 const uint8_t* in_clique, int32_t* bcnt, int32_t* bslot, int64_t* boff,
-                 int64_t* tile_buf, int64_t* total, int32_t* vsort, int32_t* vrow, MgStat* st);
+                 const uint8_t* in_clique, int32_t* bcnt, int32_t* bslot, int32_t* bbk,
+                 int64_t* boff, int64_t* tile_buf, int64_t* total, int32_t* vsort, int32_t* vrow,
+                 MgStat* st);
 // score_detections raster/reduce (rgc_score.hip): one workgroup per (pair, tile)
 struct ScoreArgs {
   const int4* boxes;          // (row start, row end, col start, col end), numpy slice bounds

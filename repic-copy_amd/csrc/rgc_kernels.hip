@@ -537,6 +537,9 @@ __global__ __launch_bounds__(1024) void k4_union_lds(int k, const int32_t* __res
     if (i + 1024 < n) { e0 = fwd_off[b0 + i + 1024]; e1 = fwd_off[b0 + i + 1025]; }
     if (c0 == c1) continue;
     has_edge[b0 + i] = 1;
+    // ri: a root of box i's set as last seen (still a root unless another thread hooked it:
+    // then the find below walks on from it), so each edge costs one find of its target
+    int ri = uf_find_l(P, i);
     for (int64_t e = c0; e < c1; e += UF_B) {
       int hs[UF_B];
 #pragma unroll
@@ -546,16 +549,19 @@ __global__ __launch_bounds__(1024) void k4_union_lds(int k, const int32_t* __res
         const int h = hs[u];
         if (h < 0) continue;
         has_edge[b0 + h] = 1;
-        int a = i, b = h;
+        int b = h;
         for (;;) {
-          a = uf_find_l(P, a);
+          ri = uf_find_l(P, ri);
           b = uf_find_l(P, b);
-          if (a == b) break;
-          if (a < b) { const int t = a; a = b; b = t; }
-          int expect = a;
-          if (__hip_atomic_compare_exchange_strong(P + a, &expect, b, __ATOMIC_RELAXED,
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+          if (ri == b) break;
+          // hook the larger root under the smaller; i's root is the smaller one afterwards
+          const int hi = ri > b ? ri : b, lo = ri > b ? b : ri;
+          int expect = hi;
+          if (__hip_atomic_compare_exchange_strong(P + hi, &expect, lo, __ATOMIC_RELAXED,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            ri = lo;
             break;
+          }
         }
       }
     }
@@ -793,36 +799,36 @@ __global__ __launch_bounds__(WG) void k7_bucket(int N, int k, const int32_t* __r
                                                 const MgGrid* __restrict__ grid,
                                                 const double* __restrict__ x,
                                                 const uint8_t* __restrict__ in_clique,
-                                                int32_t* bcnt, int32_t* bslot) {
+                                                int32_t* bcnt, int32_t* bslot, int32_t* bbk) {
   const int g = blockIdx.x * WG + threadIdx.x;
   if (g >= N || !in_clique[g]) return;
   const int m = bmg[g];
   const int b0 = box_off[m * k];
   const int bk = rank_bucket(grid[m], b0, box_off[m * k + k] - b0, x[g]);
   bslot[g] = atomicAdd(&bcnt[bk], 1);
+  bbk[g] = bk;   // (the place passes start from the bucket, not the grid lookup chain)
 }
 
 template <bool RANK>
 __global__ __launch_bounds__(WG) void k7_place(int N, int k, const int32_t* __restrict__ box_off,
                                                const int32_t* __restrict__ bmg,
-                                               const MgGrid* __restrict__ grid,
                                                const double* __restrict__ x,
                                                const double* __restrict__ y,
                                                const uint8_t* __restrict__ in_clique,
                                                const int64_t* __restrict__ boff,
-                                               const int32_t* __restrict__ bslot, int32_t* vsort,
+                                               const int32_t* __restrict__ bslot,
+                                               const int32_t* __restrict__ bbk, int32_t* vsort,
                                                int32_t* vrow) {
   const int g = blockIdx.x * WG + threadIdx.x;
   if (g >= N || !in_clique[g]) return;
-  const int m = bmg[g];
-  const int b0 = box_off[m * k];
-  const double gx = x[g];
-  const int bk = rank_bucket(grid[m], b0, box_off[m * k + k] - b0, gx);
+  const int bk = bbk[g];
   const int64_t lo = boff[bk];
   if (!RANK) {
     vsort[lo + bslot[g]] = g;
     return;
   }
+  const int b0 = box_off[bmg[g] * k];
+  const double gx = x[g];
   const int64_t hi = boff[bk + 1];
   const double gy = y[g];
   int r = (int)(lo - boff[b0]);
@@ -1023,15 +1029,16 @@ int launch_cliques_dfs(hipStream_t stream, bool fill, int N, const CliqueArgs& A
 
 void launch_rank(hipStream_t stream, int N, int n_mg, int k, const int32_t* box_off,
                  const int32_t* bmg, const MgGrid* grid, const double* x, const double* y,
-                 const uint8_t* in_clique, int32_t* bcnt, int32_t* bslot, int64_t* boff,
-                 int64_t* tile_buf, int64_t* total, int32_t* vsort, int32_t* vrow, MgStat* st) {
+                 const uint8_t* in_clique, int32_t* bcnt, int32_t* bslot, int32_t* bbk,
+                 int64_t* boff, int64_t* tile_buf, int64_t* total, int32_t* vsort, int32_t* vrow,
+                 MgStat* st) {
   const int nb = (N + WG - 1) / WG;
-  if (nb) RGC_LAUNCH(k7_bucket, nb, WG, N, k, box_off, bmg, grid, x, in_clique, bcnt, bslot);
+  if (nb) RGC_LAUNCH(k7_bucket, nb, WG, N, k, box_off, bmg, grid, x, in_clique, bcnt, bslot, bbk);
   launch_scan(stream, N, bcnt, boff, tile_buf, total);
   if (nb) {
-    RGC_LAUNCH(k7_place<false>, nb, WG, N, k, box_off, bmg, grid, x, y, in_clique, boff, bslot,
+    RGC_LAUNCH(k7_place<false>, nb, WG, N, k, box_off, bmg, x, y, in_clique, boff, bslot, bbk,
                vsort, vrow);
-    RGC_LAUNCH(k7_place<true>, nb, WG, N, k, box_off, bmg, grid, x, y, in_clique, boff, bslot,
+    RGC_LAUNCH(k7_place<true>, nb, WG, N, k, box_off, bmg, x, y, in_clique, boff, bslot, bbk,
                vsort, vrow);
   }
   RGC_LAUNCH(k7_nvert, (n_mg + WG - 1) / WG, WG, n_mg, k, box_off, boff, st);
