@@ -750,28 +750,15 @@ __global__ __launch_bounds__(WG) RGC_EPI_WPE void k5_epilogue(CliqueArgs A) {
 // members).  Wave w takes cliques [128 w, 128 w + 128) of the level route (the old epilogue's
 // balance: two per lane); every leaf prefix holds 1..64 cliques (a prefix is kept only when it
 // has a leaf), so those cliques come from at most 128 consecutive prefixes, starting at the one
-// k5_leaf_bucket recorded for the wave.  The prefixes' offsets, leaf masks, forward-list starts
-// and members are staged in LDS; lane l derives the members of cliques l and l + 64 (binary
-// search over the staged offsets, the rank-th set bit of the leaf mask, the leaf's box from
-// the root's forward list) and runs the epilogue on them.  The members never go to HBM (except
+// k5_leaf_bucket recorded for the wave.  The prefixes' forward-list starts and members are
+// staged in LDS, and each staging lane writes, for every clique of its prefix in the wave's
+// range, the prefix's slot and the leaf's lane in the root's forward list (walking the set
+// bits of the leaf mask); lane l then reads the members of cliques l and l + 64 from there
+// (two LDS bytes, the leaf's box from the root's forward list: no search) and runs the
+// epilogue on them.  The members never go to HBM (except
 // those of the ~3 % of cliques the exact pass takes): k5_leaf_fill wrote C K ints that
 // k5_epilogue read back (4 GB of traffic per C5 step of 64 micrographs).
 constexpr int LE_Q = 128;   // cliques per wave
-
-// position of the t-th (0-based) set bit of m (t < popcount(m)): six halving steps
-__device__ __forceinline__ int select_bit(uint64_t m, int t) {
-  int pos = 0;
-#pragma unroll
-  for (int w = 32; w >= 1; w >>= 1) {
-    const int c = __popcll(m & ((1ull << w) - 1));
-    if (t >= c) {
-      t -= c;
-      m >>= w;
-      pos += w;
-    }
-  }
-  return pos;
-}
 
 // bucket[b] = the leaf prefix that holds clique LE_Q b (at most one bucket start per prefix)
 __global__ __launch_bounds__(WG) void k5_leaf_bucket(LevelArgs L, int32_t* bucket) {
@@ -787,8 +774,8 @@ __global__ __launch_bounds__(WG) RGC_EPI_WPE void k5_leaf_epi(CliqueArgs A, Leve
                                                            const int32_t* bucket, int64_t C1) {
   constexpr int NWV = WG / 64;
   constexpr int NM = K - 1;                  // staged members: the root and pickers 1..K-2
-  __shared__ int32_t s_off[NWV][LE_Q];       // prefix's first clique - the wave's first
-  __shared__ uint64_t s_c[NWV][LE_Q];        // leaf masks
+  __shared__ uint8_t s_slot[NWV][LE_Q];      // clique -> its prefix's staging slot
+  __shared__ uint8_t s_lv[NWV][LE_Q];        // clique -> its leaf's lane in the root's list
   __shared__ int64_t s_lo[NWV][LE_Q];        // root's forward-list start
   __shared__ int32_t s_m[NWV][NM][LE_Q];     // the prefix's members (the same for its cliques)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -800,39 +787,38 @@ __global__ __launch_bounds__(WG) RGC_EPI_WPE void k5_leaf_epi(CliqueArgs A, Leve
   for (int h = 0; h < 2; ++h) {
     const int t = lane + 64 * h;
     const int64_t i = a0 + t;
-    int32_t o = INT_MAX;
-    uint64_t c = 0;
-    int64_t lo = 0;
     if (i < L.n_items) {
       const int64_t oi = L.off[i] - j0;
       if (oi < LE_Q) {   // (prefixes past the wave's range stay unstaged)
-        o = (int32_t)oi;
         const int r = L.in_root[i];
         const uint64_t P = L.in_P[i];
-        lo = A.fwd_off[r];
-        c = L.in_M[i];   // (the last fill stored the leaf mask itself)
+        const int64_t lo = A.fwd_off[r];
+        uint64_t c = L.in_M[i];   // (the last fill stored the leaf mask itself)
+        s_lo[wv][t] = lo;
         s_m[wv][0][t] = r;
 #pragma unroll
         for (int u = 0; u < K - 2; ++u) s_m[wv][u + 1][t] = A.e_dst[lo + ((P >> (6 * u)) & 63)];
+        // the prefix's cliques in the wave's range: slot and leaf lane by clique (the
+        // first prefix may start before the range)
+        for (int q = (int)oi; c && q < LE_Q; ++q) {
+          const int v = __builtin_ctzll(c);
+          c &= c - 1;
+          if (q >= 0) {
+            s_slot[wv][q] = (uint8_t)t;
+            s_lv[wv][q] = (uint8_t)v;
+          }
+        }
       }
     }
-    s_off[wv][t] = o;
-    s_c[wv][t] = c;
-    s_lo[wv][t] = lo;
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   // clique q: its prefix's staging slot and its leaf box
   auto locate = [&](int q, int* slot, int* leaf) {
-    // the last staged prefix whose first clique is <= q (s_off[0] <= 0)
-    int a = 0;
-#pragma unroll
-    for (int step = 64; step >= 1; step >>= 1)
-      if (a + step < LE_Q && s_off[wv][a + step] <= q) a += step;
-    const int v = select_bit(s_c[wv][a], q - s_off[wv][a]);   // the leaf's lane
+    const int a = s_slot[wv][q];
     *slot = a;
-    *leaf = A.e_dst[s_lo[wv][a] + v];
+    *leaf = A.e_dst[s_lo[wv][a] + s_lv[wv][q]];
   };
   const int qa = lane, qb = lane + 64;
   if (j0 + qa >= C1) return;
