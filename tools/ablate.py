@@ -19,7 +19,9 @@ from repic_amd.pipeline import Batch  # noqa: E402
 cfg_name = sys.argv[1] if len(sys.argv) > 1 else "C2"
 n_mg = int(sys.argv[2]) if len(sys.argv) > 2 else 10000
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 7
-cfg = synth.SynthConfig(**synth.CONFIGS[cfg_name], seed=0)
+# (C2_frac: C2 with 3-decimal coordinates, bench.py's by_config entry of that name)
+cfg = synth.SynthConfig(**synth.CONFIGS[cfg_name.replace("_frac", "")], seed=0,
+                        frac=cfg_name.endswith("_frac"))
 batch = Batch.pack(cfg.k, cfg.box, synth.batch(cfg, n_mg))
 libs = sorted(glob.glob(os.path.join(ROOT, "abl/*.so"))) + [_lib.LIB_PATH]
 if len(sys.argv) > 4:   # one library only (per-phase PMC passes: tools/gpu_pmc_ablate.sh)
