@@ -55,8 +55,10 @@ constexpr int MAXW = 16;            // reduction slots: up to 1024-thread workgr
 // Workgroup sizes compiled: 512 for every k; 768 / 1024 threads (12 / 16 waves) for k <= 5,
 // launched when LDS allows few workgroups per CU but VGPRs allow more waves (rgc_abi.cpp);
 // 256 threads for k <= 3 (fewer per-wave fixed costs per micrograph, fewer resident waves).
-// boxes per thread kept in registers from P0 to P1: 2 (4 with 256-thread workgroups)
-constexpr int fused_rb(int nt) { return nt <= 256 ? 4 : 2; }
+// boxes per thread kept in registers from P0 to P1: 2 (4 with 256-thread workgroups; 5 with
+// 1024: C3's ~4.1k boxes all stay in registers, VGPRs to spare at 4 waves per SIMD; boxes past
+// RB * NT are re-read from HBM in each of P0's and P1's passes)
+constexpr int fused_rb(int nt) { return nt <= 256 ? 4 : nt >= 1024 ? 5 : 2; }
 
 struct FusedHdr {
   // reduction scratch: the single-value reductions alias the 4-way one (every reduction
