@@ -570,6 +570,9 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   L.next_cnt = nullptr;
   int cur = 0;
   int64_t C1 = 0, C2 = 0;
+  // k >= 3 without members in the outputs: the leaf level's cliques are generated inside their
+  // epilogue (k5_leaf_epi), their members never written (the exact pass's excepted)
+  const bool leaf_epi = !want_members && !multi && k >= 3;
   for (int lv = 0; lv <= k - 2; ++lv) {
     const bool first = lv == 0, leaf = lv == k - 2;
     L.D = lv;
@@ -584,7 +587,15 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
       // (first level: L.cnt was zeroed with the per-box arrays; non-roots stay 0)
       if (launch_clique_level(s, first, leaf, false, A, L) != 0) return fail("unsupported k");
     }
-    launch_scan(s, L.n_items, L.cnt, D<int64_t>(c, D_LOFF), D<int64_t>(c, D_TILES), d_tot + 2);
+    // (the leaf level of the fused leaf epilogue: its scan also records the prefix holding
+    // each wave's first clique; C1 <= 64 n_items, so at most n_items / 2 + 1 waves)
+    int32_t* lbucket = nullptr;
+    if (leaf && leaf_epi) {
+      TRY(ensure_dev(c, D_LBUCKET, ((size_t)L.n_items / 2 + 2) * 4));
+      lbucket = D<int32_t>(c, D_LBUCKET);
+    }
+    launch_scan(s, L.n_items, L.cnt, D<int64_t>(c, D_LOFF), D<int64_t>(c, D_TILES), d_tot + 2,
+                lbucket, LEAF_Q);
     HIPCHK(hipMemcpyAsync(h_tot + 1, d_tot + 1, 16, hipMemcpyDeviceToHost, s));
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));
@@ -636,9 +647,6 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   A.conf = D<float>(c, D_CONF) + out_base;
   A.consensus = D<int32_t>(c, D_CONS) + out_base;
   A.order = multi ? D<uint8_t>(c, D_ORDER) + out_base * k : nullptr;
-  // k >= 3 without members in the outputs: the leaf level's cliques are generated inside their
-  // epilogue (k5_leaf_epi), their members never written (the exact pass's excepted)
-  const bool leaf_epi = !want_members && !multi && k >= 3;
   if (!leaf_epi) {
     TRY(mark(c, "k5_leaf_fill"));
     launch_clique_level(s, k == 2, true, true, A, L);
@@ -665,8 +673,7 @@ static int run_multi(rgc_ctx* c, int n_mg, int k, double B, double two_b2, int g
   A.epi_lo = 0;
   if (leaf_epi) {
     TRY(mark(c, "k5_leaf_epi"));
-    // (the prefix holding each wave's first clique)
-    TRY(ensure_dev(c, D_LBUCKET, ((C1 + 127) / 128 + 1) * 4));
+    // (the prefix holding each wave's first clique: written by the leaf level's scan)
     if (launch_clique_leaf_epi(s, A, L, D<int32_t>(c, D_LBUCKET), C1) != 0)
       return fail("unsupported k");
     A.epi_lo = C1;   // k5_epilogue: the DFS route's cliques only

@@ -750,7 +750,8 @@ __global__ __launch_bounds__(WG) RGC_EPI_WPE void k5_epilogue(CliqueArgs A) {
 // members).  Wave w takes cliques [128 w, 128 w + 128) of the level route (the old epilogue's
 // balance: two per lane); every leaf prefix holds 1..64 cliques (a prefix is kept only when it
 // has a leaf), so those cliques come from at most 128 consecutive prefixes, starting at the one
-// k5_leaf_bucket recorded for the wave.  The prefixes' forward-list starts and members are
+// the leaf level's scan recorded for the wave (launch_scan's bucket output, no pass of its
+// own).  The prefixes' forward-list starts and members are
 // staged in LDS, and each staging lane writes, for every clique of its prefix in the wave's
 // range, the prefix's slot and the leaf's lane in the root's forward list (walking the set
 // bits of the leaf mask); lane l then reads the members of cliques l and l + 64 from there
@@ -758,17 +759,8 @@ __global__ __launch_bounds__(WG) RGC_EPI_WPE void k5_epilogue(CliqueArgs A) {
 // epilogue on them.  The members never go to HBM (except
 // those of the ~3 % of cliques the exact pass takes): k5_leaf_fill wrote C K ints that
 // k5_epilogue read back (4 GB of traffic per C5 step of 64 micrographs).
-constexpr int LE_Q = 128;   // cliques per wave
+constexpr int LE_Q = LEAF_Q;   // cliques per wave
 
-// bucket[b] = the leaf prefix that holds clique LE_Q b (at most one bucket start per prefix)
-__global__ __launch_bounds__(WG) void k5_leaf_bucket(LevelArgs L, int32_t* bucket) {
-  const int64_t i = (int64_t)blockIdx.x * WG + threadIdx.x;
-  if (i >= L.n_items) return;
-  const int64_t lo = L.off[i], hi = L.off[i + 1];
-  for (int64_t b = (lo + LE_Q - 1) / LE_Q; b * LE_Q < hi; ++b) bucket[b] = (int32_t)i;
-}
-
-// (k = 8 at 2 waves per SIMD ran 15 % slower than at 3: profiles/r06l_*; 4: RGC_EPI_WPE_N)
 template <int K>
 __global__ __launch_bounds__(WG) RGC_EPI_WPE void k5_leaf_epi(CliqueArgs A, LevelArgs L,
                                                            const int32_t* bucket, int64_t C1) {
@@ -1003,9 +995,7 @@ int launch_clique_epilogue(hipStream_t stream, bool exact_pass, const CliqueArgs
 
 int launch_clique_leaf_epi(hipStream_t stream, const CliqueArgs& A, const LevelArgs& L,
                            int32_t* bucket, int64_t C1) {
-  const int64_t nb = (L.n_items + WG - 1) / WG;
-  if (nb <= 0 || C1 <= 0) return 0;
-  hipLaunchKernelGGL(k5_leaf_bucket, dim3(nb), dim3(WG), 0, stream, L, bucket);
+  if (L.n_items <= 0 || C1 <= 0) return 0;
   const int64_t nw = (C1 + LE_Q - 1) / LE_Q, nbe = (nw + WG / 64 - 1) / (WG / 64);
   switch (A.k) {
 #define RGC_LE(KK) \

@@ -240,8 +240,9 @@ int64_t scan_tiles_needed(int64_t n);
 // 2^22 - 1 launches)
 constexpr uint32_t SCAN_EPOCH_REFRESH = 1u << 20;
 uint64_t scan_epoch_count();
+// (bucket: also bucket[b] = the item whose output range holds position b * bq)
 void launch_scan(hipStream_t stream, int64_t n, const int32_t* in, int64_t* out,
-                 int64_t* tile_buf, int64_t* total);
+                 int64_t* tile_buf, int64_t* total, int32_t* bucket = nullptr, int bq = 1);
 void launch_cc(hipStream_t stream, int phase, int N, int n_mg, int k, int get_cc,
                const int32_t* box_off, const int32_t* bmg, const uint8_t* bpick,
                const int64_t* fwd_off, const int32_t* e_dst, int32_t* parent, uint8_t* has_edge,
@@ -268,7 +269,9 @@ int launch_clique_level(hipStream_t stream, bool first, bool leaf, bool fill, co
                         const LevelArgs& L);
 int launch_clique_epilogue(hipStream_t stream, bool exact_pass, const CliqueArgs& A);
 void launch_clique_pack(hipStream_t stream, int N, const CliqueArgs& A);
-// (bucket: (C1 + 127) / 128 int32 of scratch)
+// cliques per wave of the fused leaf epilogue; bucket[w] = the leaf prefix holding clique
+// LEAF_Q w (the leaf level's scan writes it: launch_scan's bucket output)
+constexpr int LEAF_Q = 128;
 int launch_clique_leaf_epi(hipStream_t stream, const CliqueArgs& A, const LevelArgs& L,
                            int32_t* bucket, int64_t C1);
 void launch_clique_ranges(hipStream_t stream, const CliqueArgs& A, int64_t C1, int64_t* rlo,

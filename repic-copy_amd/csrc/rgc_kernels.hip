@@ -343,7 +343,8 @@ __device__ __forceinline__ void st_store(uint64_t* p, uint64_t v) {
 
 __global__ __launch_bounds__(WG) void scan_onepass(int64_t n, const int32_t* __restrict__ in,
                                                    int64_t* __restrict__ out, int64_t* total,
-                                                   uint64_t* buf, uint32_t epoch) {
+                                                   uint64_t* buf, uint32_t epoch,
+                                                   int32_t* bucket, int bq) {
   __shared__ int64_t red[NW];
   __shared__ int64_t s_pre;
   __shared__ uint32_t s_tile;
@@ -418,6 +419,17 @@ __global__ __launch_bounds__(WG) void scan_onepass(int64_t n, const int32_t* __r
   }
   __syncthreads();
   pre += s_pre;
+  if (bucket) {
+    // (optional) bucket[b] = the item whose range [out[i], out[i + 1]) holds position b * bq,
+    // b = 0 .. total / bq: the leaf epilogue's first prefix per wave of bq cliques
+    int64_t a = pre;
+#pragma unroll
+    for (int i = 0; i < ONE_PER; ++i) {
+      const int64_t e = a + v[i];
+      for (int64_t b = (a + bq - 1) / bq; b * bq < e; ++b) bucket[b] = (int32_t)(t0 + i);
+      a = e;
+    }
+  }
   if (vec && t0 + ONE_PER <= n) {
 #pragma unroll
     for (int i = 0; i < ONE_PER; i += 2) {
@@ -964,13 +976,14 @@ static std::atomic<uint64_t> g_scan_epochs{0};
 uint64_t scan_epoch_count() { return g_scan_epochs.load(); }
 
 void launch_scan(hipStream_t stream, int64_t n, const int32_t* in, int64_t* out,
-                 int64_t* tile_buf, int64_t* total) {
+                 int64_t* tile_buf, int64_t* total, int32_t* bucket, int bq) {
   // launch epochs are process-wide (any two launches sharing a tile buffer differ; an epoch
   // repeats after 2^22 - 1 launches, so the owner of a tile buffer zeroes it at least every
   // SCAN_EPOCH_REFRESH launches: scan_epoch_count)
   const uint32_t e = (uint32_t)(g_scan_epochs.fetch_add(1) % ((1u << 22) - 1)) + 1;
   const int64_t nt = std::max<int64_t>(1, (n + ONE_TILE - 1) / ONE_TILE);
-  RGC_LAUNCH(scan_onepass, nt, WG, n, in, out, total, reinterpret_cast<uint64_t*>(tile_buf), e);
+  RGC_LAUNCH(scan_onepass, nt, WG, n, in, out, total, reinterpret_cast<uint64_t*>(tile_buf), e,
+             bucket, bq);
 }
 
 void launch_cc(hipStream_t stream, int phase, int N, int n_mg, int k, int get_cc,
