@@ -70,10 +70,11 @@ def fixed_shard(total, world, rank):
 
 def stream_plan(depth):
     """Streams (hardware queues) one bench process uses: a launch stream per context in flight
-    plus the null stream (torch's default; the library copies non-lazy per-micrograph stats
-    on it, rgc_ctx_set_copy_stream(ctx, 0)), no other copy stream.  Must fit HW_QUEUES, or
-    streams share queues in creation order (round 5: the stats-copy variant ran 68 % slower
-    on the driver's box with 7 streams)."""
+    plus the null stream (torch's default; rgc_ctx_set_copy_stream(ctx, 0) for any copy the
+    library issues off the launch stream; non-lazy runs' stats come from the ties kernel on
+    the launch stream), no other copy stream.  Must fit HW_QUEUES, or streams share queues in
+    creation order (round 5: the stats-copy variant ran 68 % slower on the driver's box with 7
+    streams)."""
     plan = {"launch_streams": depth, "null_stream": 1, "copy_streams": 0}
     plan["total"] = plan["launch_streams"] + plan["null_stream"] + plan["copy_streams"]
     assert plan["total"] <= HW_QUEUES, plan
@@ -480,7 +481,9 @@ def measure(args, env, config, n_mg, steps, warmup, host_io=False, no_pipeline=F
                         for j in range(1, depth)]
     else:
         ctxs = [ctx, _lib.Context(env.local, stream)] if pipeline else [ctx]
-    for c in ctxs:   # non-lazy stats copies on the null stream: no extra hardware queue
+    # (non-lazy runs get their stats from the ties kernel on the launch stream; any copy the
+    # library still issues goes to the null stream: no extra hardware queue)
+    for c in ctxs:
         c.set_copy_stream(0)
 
     def step(timing=False):

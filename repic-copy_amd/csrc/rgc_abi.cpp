@@ -843,7 +843,7 @@ static int run_impl(rgc_ctx* c, const rgc_batch_in* in, rgc_batch_out* out) {
       TRY(fused_io(c, n_mg, cur_off, &io));
       if (attempt > 0) HIPCHK(hipMemsetAsync(io.cur, 0, CUR_BYTES, s));
       h_cur = io.h_cur;
-      FusedArgs A;
+      FusedArgs A{};
       A.k = k; A.flags = get_cc | (multi << 1) | (want_members ? 32 : 0);
       A.B = B; A.two_b2 = two_b2;
       A.box_off = d_bo; A.id_base = d_id;
@@ -1212,7 +1212,7 @@ static int submit_fast(rgc_ctx* c, const rgc_batch_in* in) {
   TRY(ensure_outputs(c, c->cap_cliques, 0, k, want_members, multi));
   FusedIo io;
   TRY(fused_io(c, n_mg, cur_off, &io));
-  FusedArgs A;
+  FusedArgs A{};
   A.k = k;
   A.flags = ((flags & RGC_F_GET_CC) ? 1 : 0) | (multi ? 2 : 0) | (want_members ? 32 : 0);
   A.B = (double)in->box_size;
@@ -1286,6 +1286,14 @@ static int submit_fast(rgc_ctx* c, const rgc_batch_in* in) {
     if (le != 0) return fail("fused f64 kernel launch failed (submit): " +
                              std::string(le > 0 ? hipGetErrorString((hipError_t)le) : "unsupported k"));
   }
+  // every micrograph's stats to the host from the ties kernel (the run's last kernel) when
+  // the caller wants them with every run
+  const bool stats_in_ties = !(flags & RGC_F_LAZY_STATS) && A.tie_list && A.tie_cap > 0;
+  if (stats_in_ties) {
+    A.stats_dev = D<char>(c, D_MGOUT);
+    A.host_stats = H<char>(c, H_MGOUT);
+    A.stats_bytes = (int64_t)cur_off;
+  }
   TRY(mark(c, "k_fused_ties"));
   if (launch_fused_ties(s, A, 0) != 0) return fail("tie kernel launch failed (submit)");
   c->pend_slot = io.slot;
@@ -1298,11 +1306,17 @@ static int submit_fast(rgc_ctx* c, const rgc_batch_in* in) {
   // THIS context is submitted after rgc_wait, and other contexts launch on streams of their
   // own (bench.py: one stream per context), whose hardware queues a side copy stream per
   // context would share (3-4 % with two or three contexts in flight,
-  // profiles/r05w_ab_copy_on_stream.txt).  Every micrograph's stats (48 B each) on the
-  // context's side copy stream after an event: as a blit kernel on the launch stream that copy
-  // waits for CUs behind the other contexts' workgroups (C2: 0.39 -> 0.56 ms per step).
+  // profiles/r05w_ab_copy_on_stream.txt).  Every micrograph's stats (48 B each): written to
+  // the pinned host block by the ties kernel itself (stats_in_ties).  As a copy they were a
+  // blit kernel: on the launch stream it waited for CUs behind the other contexts'
+  // workgroups (C2: 0.39 -> 0.56 ms per step), on a side stream after an event its wait
+  // packet sat in a hardware queue that, depending on how a process's streams mapped onto
+  // the 4 queues, a launch stream could share (14.3-14.8 M against 25 M micrographs/s on
+  // half the processes measured, profiles/r06az_*).
   if (!c->ev_sub) HIPCHK(hipEventCreateWithFlags(&c->ev_sub, hipEventDisableTiming));
-  if (flags & RGC_F_LAZY_STATS) {   // the run's totals only; rgc_fetch_stats copies the rest
+  if (stats_in_ties) {
+    HIPCHK(hipEventRecord(c->ev_sub, s));
+  } else if (flags & RGC_F_LAZY_STATS) {   // the run's totals only; rgc_fetch_stats copies the rest
     const size_t so = cur_off + (size_t)io.slot * CUR_BYTES;
     HIPCHK(hipMemcpyAsync(H<char>(c, H_MGOUT) + so, D<char>(c, D_MGOUT) + so, CUR_BYTES,
                           hipMemcpyDeviceToHost, s));
