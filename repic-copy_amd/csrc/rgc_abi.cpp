@@ -1314,9 +1314,9 @@ static int submit_fast(rgc_ctx* c, const rgc_batch_in* in) {
   // the 4 queues, a launch stream could share (14.3-14.8 M against 25 M micrographs/s on
   // half the processes measured, profiles/r06az_*).
   if (!c->ev_sub) HIPCHK(hipEventCreateWithFlags(&c->ev_sub, hipEventDisableTiming));
-  if (stats_in_ties) {
-    HIPCHK(hipEventRecord(c->ev_sub, s));
-  } else if (flags & RGC_F_LAZY_STATS) {   // the run's totals only; rgc_fetch_stats copies the rest
+  if (stats_in_ties || (flags & RGC_F_LAZY_STATS)) {
+    // the run's totals (a lazy run's other stats: rgc_fetch_stats; a non-lazy run's: the
+    // ties kernel wrote them)
     const size_t so = cur_off + (size_t)io.slot * CUR_BYTES;
     HIPCHK(hipMemcpyAsync(H<char>(c, H_MGOUT) + so, D<char>(c, D_MGOUT) + so, CUR_BYTES,
                           hipMemcpyDeviceToHost, s));

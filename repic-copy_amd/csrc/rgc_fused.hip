@@ -2027,29 +2027,13 @@ __global__ __launch_bounds__(256) void k_fused_ties(FusedArgs A, int64_t from) {
     }
   }
   if (A.host_stats) {
-    // the per-micrograph stats to the host (final: the fused launches before this one wrote
-    // them), every workgroup a slice; then the cursor slot, by the last workgroup to finish
-    // (after every workgroup's cursor atomics above)
+    // the per-micrograph stats to the host, every workgroup a slice (final: the fused launches
+    // before this one wrote them; the kernel's end makes the writes visible to the host)
     const int64_t n16 = A.stats_bytes / 16;
     const uint4* src = reinterpret_cast<const uint4*>(A.stats_dev);
     uint4* dst = reinterpret_cast<uint4*>(A.host_stats);
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256)
       dst[i] = src[i];
-    __shared__ int last;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __threadfence();
-      last = atomicAdd(A.cursor + CUR_TIES_DONE, 1ull) == (unsigned long long)gridDim.x - 1;
-      __threadfence();
-    }
-    __syncthreads();
-    if (last && threadIdx.x < 16) {
-      unsigned long long* hc = reinterpret_cast<unsigned long long*>(
-          A.host_stats + (reinterpret_cast<const char*>(A.cursor) - A.stats_dev));
-      hc[threadIdx.x] = __hip_atomic_load(A.cursor + threadIdx.x, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __threadfence_system();
   }
 }
 

@@ -144,15 +144,12 @@ struct FusedArgs {
   int32_t* wide_list;
   const unsigned long long* mg_count;
   // rgc_submit without lazy stats: k_fused_ties, the run's last kernel, writes the
-  // per-micrograph block [stats_dev, stats_dev + stats_bytes) to host_stats (pinned) and, from
-  // its last workgroup, the run's cursor slot after it: the host reads the stats after the
-  // run's event, with no copy packet (a blit kernel) on another stream's hardware queue
+  // per-micrograph block [stats_dev, stats_dev + stats_bytes) to host_stats (pinned), so
+  // only the run's 128-B cursor slot is copied, on the launch stream, as for a lazy run
   const char* stats_dev;
   char* host_stats;   // nullptr: none
   int64_t stats_bytes;
 };
-// cursor-slot word counting k_fused_ties' finished workgroups (its last one copies the slot)
-constexpr int CUR_TIES_DONE = 7;
 
 int fused_lds_bytes(int nmax, int ecap, bool wide);
 int fused_vgprs(int k, bool wide, int nt);
